@@ -1,0 +1,81 @@
+"""ctypes binding of the HIP C ABI (include/dg_advec.h).
+
+There is no CPU fallback: if ``lib/libdgadv.so`` is missing or fails to load, every
+entry point raises :class:`DGLibraryError`.  Build it with ``__graft_entry__.build()``
+(or ``python -m`` the package's ``build_ext``).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdgadv.so")
+HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "include", "dg_advec.h"))
+
+# Enumerations of include/dg_advec.h
+DG_OK, DG_ERR_ARG, DG_ERR_HIP, DG_ERR_NOMEM = 0, -1, -2, -3
+DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T = 0, 1
+DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
+
+_c_dbl_p = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+
+# name -> (restype, argtypes); device pointers are passed as c_void_p integers.
+SIGNATURES = {
+    "dg_last_error": (ctypes.c_char_p, []),
+    "dg_version": (ctypes.c_char_p, []),
+    "dg_plan_create": (_i32, [_i32, _i64, _i64, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p,
+                              _c_dbl_p, ctypes.c_double, _i32, _i32, ctypes.POINTER(_vp)]),
+    "dg_plan_destroy": (_i32, [_vp]),
+    "dg_plan_query": (_i32, [_vp, ctypes.POINTER(_i64)]),
+    "dg_advec_rhs": (_i32, [_vp, _vp, _vp, ctypes.c_double, _vp]),
+    "dg_lserk4_fwd": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp]),
+    "dg_lserk4_adj": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32,
+                             ctypes.c_double, _vp, _vp]),
+    "dg_slope_limit_n": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "dg_argmax": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "dg_sum_rows": (_i32, [_vp, _i64, _i64, _vp, _vp]),
+    "dg_init_sine": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
+}
+
+
+class DGLibraryError(RuntimeError):
+  """The HIP extension is missing, failed to load, or a call returned an error code."""
+
+
+_lib = None
+
+
+def load():
+  """Load the shared library once; raise loudly if it is absent (no fallback)."""
+  global _lib
+  if _lib is not None:
+    return _lib
+  if not os.path.exists(LIB_PATH):
+    raise DGLibraryError(
+        f"HIP extension not built: {LIB_PATH} is missing. Run `python -c \"import "
+        f"__graft_entry__; __graft_entry__.build()\"` from the repository root.")
+  try:
+    lib = ctypes.CDLL(LIB_PATH)
+  except OSError as e:
+    raise DGLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+  for name, (res, args) in SIGNATURES.items():
+    fn = getattr(lib, name)
+    fn.restype = res
+    fn.argtypes = args
+  _lib = lib
+  return lib
+
+
+def check(rc, what=""):
+  if rc != DG_OK:
+    msg = load().dg_last_error().decode(errors="replace")
+    raise DGLibraryError(f"{what} failed with code {rc}: {msg}")
+
+
+def dbl_array(values):
+  """Host float64 buffer for the plan-creation arguments."""
+  import numpy as np
+  arr = np.ascontiguousarray(values, dtype=np.float64)
+  return arr, arr.ctypes.data_as(_c_dbl_p)

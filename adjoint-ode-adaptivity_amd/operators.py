@@ -1,0 +1,196 @@
+"""GPU DG advection operator: the Python face of the HIP plan (include/dg_advec.h).
+
+``DGAdvection1D`` replaces the MATLAB global-state calls of the reference hot path:
+
+=================================  ===============================================
+reference                           here
+=================================  ===============================================
+``AdvecRHS1D(u, t, a)``             ``op.rhs(u, t)``          (utils/AdvecRHS1D.m:1)
+LSERK4 loop, One_code.mlx:106-140   ``op.forward(u, t0, dt, nsteps, snapshots)``
+``adj_march`` / adjSolve role       ``op.adjoint(w, snapshots, t0, dt, nsteps, ...)``
+``err_contribution`` / errEst role  the ``eta`` output of ``op.adjoint``
+``SlopeLimitN(u)``                  ``op.slope_limit(u)``      (utils/SlopeLimitN.m:1)
+``argmax(err)`` (:337)              ``op.argmax(eta, use_abs=True)``
+=================================  ===============================================
+
+Tensors are torch CUDA float64 tensors in the device layout (element-major,
+``u[(b*K + k)*Np + i]``); any shape with that many contiguous elements is accepted.
+Work is enqueued on torch's current stream.  There is no CPU path: a CPU tensor or a
+missing library raises.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .galerkin import BaseGalerkin1D
+
+INFLOW = {"a": _lib.DG_INFLOW_SIN_AT, "a2": _lib.DG_INFLOW_SIN_A2T}
+SCHEME = {"lserk4": _lib.DG_TIME_LSERK4, "euler": _lib.DG_TIME_EULER}
+
+
+def _stream(device):
+  return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class DGAdvection1D:
+  """A plan for ``batch`` trajectories of 1D linear advection on one nodal-DG mesh.
+
+  Args:
+    mesh: a :class:`BaseGalerkin1D` (its ``r_gl``, ``v``, ``inv_v``, ``d_r``, ``lift``,
+      ``v_x`` are handed to the plan), or an int polynomial order together with ``v_x``.
+    a: advection speed (One_code.mlx:116 uses 2*pi).
+    batch: independent trajectories (ensemble ICs) sharing the mesh.
+    inflow: "a" (uin = -sin(a t), AdvecRHS1D.m:14) or "a2" (-sin(a^2 t), One_code.mlx:129).
+    time_scheme: "lserk4" (Globals1D.m:19-34) or "euler".
+  """
+
+  def __init__(self, mesh, a=2 * np.pi, batch=1, inflow="a", time_scheme="lserk4",
+               v_x=None, device=None):
+    if not isinstance(mesh, BaseGalerkin1D):
+      mesh = BaseGalerkin1D(n=int(mesh), v_x=v_x)
+    if not torch.cuda.is_available():
+      raise _lib.DGLibraryError("DGAdvection1D needs a ROCm GPU (torch.cuda is unavailable)")
+    self.mesh = mesh
+    self.a = float(a)
+    self.batch = int(batch)
+    self.inflow = inflow
+    self.time_scheme = time_scheme
+    self.N = mesh.n
+    self.Np = mesh.n_p
+    self.K = mesh.k
+    self.ktot = self.K * self.batch
+    self.field_numel = self.ktot * self.Np
+    self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    lib = _lib.load()
+    keep = [_lib.dbl_array(x) for x in (mesh.r_gl, mesh.v, mesh.inv_v, mesh.d_r, mesh.lift,
+                                        mesh.v_x)]
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(self.device):
+      rc = lib.dg_plan_create(self.N, self.K, self.batch, *[p for _, p in keep], self.a,
+                              INFLOW[inflow], SCHEME[time_scheme], ctypes.byref(handle))
+    _lib.check(rc, "dg_plan_create")
+    self._plan = handle
+    self._lib = lib
+    q = (ctypes.c_int64 * 6)()
+    _lib.check(lib.dg_plan_query(self._plan, q), "dg_plan_query")
+    self.uniform = bool(q[4])
+    self.stages = int(q[5])
+    self._idx = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+  # --- lifetime ---
+  def close(self):
+    if getattr(self, "_plan", None):
+      self._lib.dg_plan_destroy(self._plan)
+      self._plan = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:  # interpreter shutdown
+      pass
+
+  def __enter__(self):
+    return self
+
+  def __exit__(self, *exc):
+    self.close()
+
+  # --- checks ---
+  def _field(self, t, name, numel=None, dtype=torch.float64):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+      raise TypeError(f"{name} must be a CUDA tensor (no CPU path)")
+    if t.dtype != dtype:
+      raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+      raise ValueError(f"{name} must be contiguous")
+    want = self.field_numel if numel is None else numel
+    if t.numel() != want:
+      raise ValueError(f"{name} has {t.numel()} elements, expected {want}")
+    return ctypes.c_void_p(t.data_ptr())
+
+  def new_field(self, count=None):
+    shape = (self.field_numel,) if count is None else (count, self.field_numel)
+    return torch.empty(shape, dtype=torch.float64, device=self.device)
+
+  # --- kernels ---
+  def rhs(self, u, t, out=None):
+    """AdvecRHS1D(u, t, a) (utils/AdvecRHS1D.m:1-20)."""
+    out = torch.empty_like(u) if out is None else out
+    rc = self._lib.dg_advec_rhs(self._plan, self._field(u, "u"), self._field(out, "out"),
+                                float(t), _stream(self.device))
+    _lib.check(rc, "dg_advec_rhs")
+    return out
+
+  def forward(self, u, t0, dt, nsteps, snapshots=None):
+    """nsteps fused steps in place on u (One_code.mlx:119-140); optional snapshots
+    ((nsteps+1) * field) receive u^0..u^nsteps."""
+    snap_p = None
+    if snapshots is not None:
+      snap_p = self._field(snapshots, "snapshots", (nsteps + 1) * self.field_numel)
+    rc = self._lib.dg_lserk4_fwd(self._plan, self._field(u, "u"), float(t0), float(dt),
+                                 int(nsteps), snap_p, _stream(self.device))
+    _lib.check(rc, "dg_lserk4_fwd")
+    return u
+
+  def adjoint(self, w, snapshots, t0, dt, nsteps, src_coef=0.0, eta=None):
+    """Discrete adjoint sweep in place on w (terminal dJ/du^N in, dJ/du^0 out) and the
+    dual-weighted residual accumulated into eta (batch*K, caller-zeroed)."""
+    eta_p = None if eta is None else self._field(eta, "eta", self.ktot)
+    rc = self._lib.dg_lserk4_adj(self._plan, self._field(w, "w"),
+                                 self._field(snapshots, "snapshots",
+                                             (nsteps + 1) * self.field_numel),
+                                 float(t0), float(dt), int(nsteps), float(src_coef), eta_p,
+                                 _stream(self.device))
+    _lib.check(rc, "dg_lserk4_adj")
+    return w, eta
+
+  def slope_limit(self, u, out=None, ids=None):
+    """SlopeLimitN(u) (utils/SlopeLimitN.m:1-33); ids (int32, batch*K) marks limited cells."""
+    out = torch.empty_like(u) if out is None else out
+    ids_p = None if ids is None else self._field(ids, "ids", self.ktot, torch.int32)
+    rc = self._lib.dg_slope_limit_n(self._plan, self._field(u, "u"), self._field(out, "out"),
+                                    ids_p, _stream(self.device))
+    _lib.check(rc, "dg_slope_limit_n")
+    return out
+
+  def argmax_async(self, x, use_abs=True, out=None):
+    """Device-side argmax (numpy semantics) into a 1-element int64 tensor."""
+    out = self._idx if out is None else out
+    n = x.numel()
+    if not x.is_cuda or x.dtype != torch.float64 or not x.is_contiguous():
+      raise TypeError("x must be a contiguous CUDA float64 tensor")
+    rc = self._lib.dg_argmax(self._plan, ctypes.c_void_p(x.data_ptr()), n, int(use_abs),
+                             ctypes.c_void_p(out.data_ptr()), _stream(self.device))
+    _lib.check(rc, "dg_argmax")
+    return out
+
+  def argmax(self, x, use_abs=True):
+    return int(self.argmax_async(x, use_abs).item())
+
+  def init_sine(self, amp, freq, phase, out=None):
+    """u_b(x) = amp[b] sin(2 pi freq[b] x + phase[b]) on the device (ensemble ICs)."""
+    out = self.new_field() if out is None else out
+    vals = [torch.as_tensor(np.asarray(v, dtype=np.float64), device=self.device)
+            for v in (amp, freq, phase)]
+    for v in vals:
+      if v.numel() != self.batch:
+        raise ValueError("amp/freq/phase need one value per trajectory")
+    rc = self._lib.dg_init_sine(self._plan, *[ctypes.c_void_p(v.data_ptr()) for v in vals],
+                                self._field(out, "u"), _stream(self.device))
+    _lib.check(rc, "dg_init_sine")
+    return out
+
+
+def sum_rows(x, rows, out=None):
+  """out[k] = sum_r x[r, k] in ascending r (dg_sum_rows)."""
+  lib = _lib.load()
+  if not x.is_cuda or x.dtype != torch.float64 or not x.is_contiguous():
+    raise TypeError("x must be a contiguous CUDA float64 tensor")
+  n = x.numel() // rows
+  out = torch.empty(n, dtype=torch.float64, device=x.device) if out is None else out
+  rc = lib.dg_sum_rows(ctypes.c_void_p(x.data_ptr()), int(rows), int(n),
+                       ctypes.c_void_p(out.data_ptr()), _stream(x.device))
+  _lib.check(rc, "dg_sum_rows")
+  return out

@@ -1,0 +1,128 @@
+/*
+ * dg_advec.h — C ABI of the MI355X-native forward + adjoint DG advection time-stepper.
+ *
+ * The reference (wglao/Adjoint-ODE-Adaptivity) has no FFI: its hot path is a set of
+ * MATLAB global-state functions (utils/AdvecRHS1D.m, utils/SlopeLimitN.m, utils/minmod.m),
+ * an inlined LSERK4 loop (utils/One_code.mlx:106-140) and the DWR/refine pattern of
+ * python/Main_finite_difference.py:54-94,336-341.  Each entry point below names the
+ * reference interface it replaces.  A Python caller binds it with ctypes
+ * (adjoint-ode-adaptivity_amd/_lib.py; stub in INTEGRATION.md).
+ *
+ * Conventions
+ *  - Layout: element-major fp64, u[e*Np + i] with e = b*K + k (trajectory b, element k),
+ *    byte-identical to MATLAB's Np x K column-major array for one trajectory.
+ *  - All array arguments of compute calls are DEVICE pointers owned by the caller.  The
+ *    library never frees caller memory and never allocates inside compute calls; scratch
+ *    lives in the plan.  Host pointers appear only in dg_plan_create (copied).
+ *  - Every function returns 0 (DG_OK) or a negative DG_ERR_* code; dg_last_error() gives
+ *    the message of the last failure on the calling thread.  No exception crosses the ABI.
+ *  - Compute calls are asynchronous on `stream` (a hipStream_t, NULL = default stream);
+ *    the caller synchronises.  A plan may be shared by threads that use different streams
+ *    for dg_advec_rhs / dg_slope_limit_n; dg_lserk4_fwd / dg_lserk4_adj / dg_argmax use
+ *    plan scratch and must not run concurrently on one plan.
+ */
+#ifndef DG_ADVEC_H
+#define DG_ADVEC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dg_plan dg_plan;
+
+enum {
+  DG_OK = 0,
+  DG_ERR_ARG = -1,         /* invalid argument (null pointer, bad size, unsupported N) */
+  DG_ERR_HIP = -2,         /* a HIP runtime call failed (message has hipGetErrorString) */
+  DG_ERR_NOMEM = -3        /* device allocation failed in dg_plan_create */
+};
+
+/* Inflow boundary value at x = 0.
+ *   DG_INFLOW_SIN_AT : uin = -sin(a*t)    utils/AdvecRHS1D.m:14
+ *   DG_INFLOW_SIN_A2T: uin = -sin(a*a*t)  utils/One_code.mlx:129 (the executed golden run) */
+enum { DG_INFLOW_SIN_AT = 0, DG_INFLOW_SIN_A2T = 1 };
+
+/* Time integrator of the forward step and of its discrete adjoint.
+ *   DG_TIME_LSERK4: 5-stage low-storage RK4, coefficients utils/Globals1D.m:19-34
+ *   DG_TIME_EULER : forward Euler u += dt*rhs (config 1 plumbing, Main_finite_difference.py:131-132 pattern) */
+enum { DG_TIME_LSERK4 = 0, DG_TIME_EULER = 1 };
+
+/* Last error message of the calling thread ("" if none). */
+const char* dg_last_error(void);
+
+/* Library version string. */
+const char* dg_version(void);
+
+/* Create an immutable plan (replaces the MATLAB globals set by utils/StartUp1D.m:5-39 and
+ * utils/Globals1D.m:3-34, and the python/galerkin.py:199-237 startUp1D attribute set).
+ *   N       polynomial order, 1..8 (Np = N+1 nodes per element)
+ *   K       elements per trajectory;  batch  independent trajectories (ensemble ICs) sharing the mesh
+ *   r, V, invV, Dr, LIFT   host arrays from the host setup (JacobiGL/Vandermonde1D/Dmatrix1D/Lift1D):
+ *           r[Np], V/invV/Dr row-major [Np][Np], LIFT row-major [Np][2]
+ *   VX      host array of K+1 vertex coordinates (utils/MeshGen1D.m:4-14, or a refined mesh)
+ *   a       advection speed; inflow_variant DG_INFLOW_*; time_scheme DG_TIME_*
+ * The metric rx = Fscale = 2/h_k is taken per element from VX (uniform meshes use one scalar). */
+int dg_plan_create(int N, int64_t K, int64_t batch,
+                   const double* r, const double* V, const double* invV,
+                   const double* Dr, const double* LIFT, const double* VX,
+                   double a, int inflow_variant, int time_scheme, dg_plan** out);
+
+/* Destroy a plan (frees its device scratch).  NULL is a no-op. */
+int dg_plan_destroy(dg_plan* plan);
+
+/* Query plan sizes: out[0]=N, out[1]=Np, out[2]=K, out[3]=batch, out[4]=uniform mesh (0/1),
+ * out[5]=time stages per step. */
+int dg_plan_query(const dg_plan* plan, int64_t out[6]);
+
+/* rhs = AdvecRHS1D(u, t, a)   — utils/AdvecRHS1D.m:1-20 (inline copy One_code.mlx:124-134).
+ * Central flux (alpha = 1), inflow at each trajectory's x = 0, du = 0 at the outflow face. */
+int dg_advec_rhs(const dg_plan* plan, const double* u, double* rhs, double t, void* stream);
+
+/* Forward sweep: nsteps fused steps of the plan's integrator starting at time t0
+ * (the "dg_march" role; LSERK4 loop One_code.mlx:106-140, time = time + dt as there).
+ * u (in/out): the state.  snapshots (nullable): (nsteps+1) consecutive states,
+ * snapshots[n] = u^n; u may alias snapshots (then u^0 is not copied). */
+int dg_lserk4_fwd(dg_plan* plan, double* u, double t0, double dt, int nsteps,
+                  double* snapshots, void* stream);
+
+/* Adjoint sweep + dual-weighted residual (the "adj_march" / "adjoint_sens" / "err_contribution"
+ * role; discrete-adjoint pattern python/Main_finite_difference.py:54-76, indicator pattern :79-94).
+ * Exact discrete transpose of the forward step, run for n = nsteps-1 .. 0:
+ *   w^{n+1} += src_coef * u^{n+1}   (functional source, left-endpoint rule: none at n+1 = nsteps)
+ *   eta[e]  += dt * sum_i w^{n+1}[e,i] * R(u^{n+1}, t_{n+1})[e,i]
+ *              R = LIFT*(Fscale.*du): the interelement-jump (strong-form) residual of AdvecRHS1D
+ *   w^n      = S^T w^{n+1}
+ * and finally w^0 += src_coef * u^0.
+ *   w (in/out): terminal dJ/du^N on entry, dJ/du^0 on exit.
+ *   snapshots : the (nsteps+1) forward states written by dg_lserk4_fwd.
+ *   eta (nullable): batch*K accumulators (caller zeroes them). */
+int dg_lserk4_adj(dg_plan* plan, double* w, const double* snapshots, double t0, double dt,
+                  int nsteps, double src_coef, double* eta, void* stream);
+
+/* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
+ * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */
+int dg_slope_limit_n(dg_plan* plan, const double* u, double* ulim, int32_t* ids_mask,
+                     void* stream);
+
+/* idx[0] = argmax(x[0:n]) (or of |x| when use_abs), first index on ties, NaN counts as
+ * maximum — numpy.argmax semantics used at python/Main_finite_difference.py:337.
+ * idx is a device int64.  n <= batch*K of the plan (scratch is sized by it). */
+int dg_argmax(dg_plan* plan, const double* x, int64_t n, int use_abs, int64_t* idx,
+              void* stream);
+
+/* out[k] = sum_{r=0}^{rows-1} x[r*n + k], summed in ascending r (bit-reproducible).
+ * Ensemble reduction of per-IC indicators (python/Main_width_ref.py:479 mean-over-ICs role). */
+int dg_sum_rows(const double* x, int64_t rows, int64_t n, double* out, void* stream);
+
+/* Synthetic ensemble initial conditions u_b(x) = amp[b] * sin(2*pi*freq[b]*x + phase[b])
+ * on the plan's mesh (amp/freq/phase: device arrays of length batch). */
+int dg_init_sine(const dg_plan* plan, const double* amp, const double* freq,
+                 const double* phase, double* u, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DG_ADVEC_H */

@@ -1,0 +1,327 @@
+"""HIP path vs the CPU oracle, through the C ABI (ctypes).  Needs an MI355X.
+
+Inputs are identical on both sides: the oracle runs with the plan's per-element metric
+(oracle.setup1d.startup1d(metric="element")), and the adjoint/indicator oracle is fed
+the GPU's own forward snapshots (the jump residual of a smooth solution is a
+cancellation-limited difference, so it is compared on the same states; the forward
+states themselves are compared separately).
+
+Tolerances (north_star: fp64 state and indicator within 1e-10 relative; integer
+outputs bit-exact):
+  * fp64 fields: max|gpu - oracle| <= RTOL * max|oracle|, RTOL = 1e-10;
+  * limiter troubled-cell ids, argmax indices, ensemble row sums: exact.
+"""
+import numpy as np
+import pytest
+
+from oracle import adjoint as oadj
+from oracle import advec as oadv
+from oracle import limiter as olim
+from oracle import setup1d
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-10
+A = 2 * np.pi
+
+
+def rel_err(x, ref):
+  x, ref = np.asarray(x), np.asarray(ref)
+  return float(np.max(np.abs(x - ref)) / max(np.max(np.abs(ref)), 1e-300))
+
+
+def mesh_pair(pkg, N, K, v_x=None, xmin=0.0, xmax=1.0):
+  if v_x is None:
+    _, v_x, _, _ = setup1d.mesh_gen1d(xmin, xmax, K)
+  S = setup1d.startup1d(N, v_x, metric="element")  # the plan's per-element rx = 2/h
+  mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+  return S, mesh
+
+
+def dev(x, device):
+  import torch
+  return torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=device)
+
+
+def host(t):
+  return t.detach().cpu().numpy()
+
+
+def make_op(pkg, mesh, **kw):
+  return pkg.operators.DGAdvection1D(mesh, **kw)
+
+
+def random_field(rng, Np, K):
+  return rng.standard_normal((Np, K))
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("inflow", ["a", "a2"])
+def test_rhs_matches_AdvecRHS1D(pkg, gpu, N, inflow):
+  rng = np.random.default_rng(N)
+  S, mesh = mesh_pair(pkg, N, 37)
+  u = random_field(rng, N + 1, 37)
+  op = make_op(pkg, mesh, inflow=inflow)
+  got = host(op.rhs(dev(setup1d.to_elem_major(u), gpu), 0.37))
+  ref, _ = oadv.advec_rhs1d(u, 0.37, A, S, inflow)
+  assert rel_err(setup1d.from_elem_major(got, N + 1), ref) <= RTOL
+
+
+def test_rhs_nonuniform_mesh(pkg, gpu):
+  rng = np.random.default_rng(7)
+  v_x = np.concatenate(([0.0], np.cumsum(rng.uniform(0.5, 1.5, 60))))
+  v_x = v_x / v_x[-1]
+  S, mesh = mesh_pair(pkg, 4, 60, v_x=v_x)
+  op = make_op(pkg, mesh)
+  assert not op.uniform
+  u = random_field(rng, 5, 60)
+  got = host(op.rhs(dev(setup1d.to_elem_major(u), gpu), 0.1))
+  ref, _ = oadv.advec_rhs1d(u, 0.1, A, S)
+  assert rel_err(setup1d.from_elem_major(got, 5), ref) <= RTOL
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("N,K", [(1, 300), (2, 513), (4, 1000), (4, 246), (6, 250), (8, 777)])
+def test_forward_sweep_matches_lserk4_loop(pkg, gpu, N, K):
+  import torch
+  S, mesh = mesh_pair(pkg, N, K)
+  u0 = np.sin(2 * np.pi * S["x"])
+  dt = oadv.bench_dt(S)
+  nsteps = 7
+  ref, _ = oadv.forward_sweep(u0, 0.05, dt, nsteps, A, S)
+  op = make_op(pkg, mesh)
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  snaps = op.new_field(nsteps + 1)
+  op.forward(u, 0.05, dt, nsteps, snaps)
+  torch.cuda.synchronize()
+  for n in range(nsteps + 1):
+    assert rel_err(setup1d.from_elem_major(host(snaps[n]), N + 1), ref[n]) <= RTOL, n
+  assert rel_err(setup1d.from_elem_major(host(u), N + 1), ref[-1]) <= RTOL
+
+
+@pytest.mark.parametrize("nsteps", [1, 2, 5, 6])
+def test_forward_without_snapshots_pingpong(pkg, gpu, nsteps):
+  S, mesh = mesh_pair(pkg, 4, 500)
+  u0 = np.cos(3 * np.pi * S["x"])
+  dt = oadv.bench_dt(S)
+  ref, _ = oadv.forward_sweep(u0, 0.0, dt, nsteps, A, S)
+  op = make_op(pkg, mesh)
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  op.forward(u, 0.0, dt, nsteps)
+  assert rel_err(setup1d.from_elem_major(host(u), 5), ref[-1]) <= RTOL
+
+
+def test_forward_nonuniform_and_euler(pkg, gpu):
+  rng = np.random.default_rng(3)
+  v_x = np.concatenate(([0.0], np.cumsum(rng.uniform(0.3, 1.7, 400))))
+  v_x = v_x / v_x[-1]
+  S, mesh = mesh_pair(pkg, 3, 400, v_x=v_x)
+  u0 = np.sin(2 * np.pi * S["x"]) + 0.1 * rng.standard_normal(S["x"].shape)
+  dt = 0.2 * oadv.bench_dt(S)
+  for scheme in ("lserk4", "euler"):
+    ref, _ = oadv.forward_sweep(u0, 0.0, dt, 4, A, S, scheme=scheme)
+    op = make_op(pkg, mesh, time_scheme=scheme)
+    u = dev(setup1d.to_elem_major(u0), gpu)
+    op.forward(u, 0.0, dt, 4)
+    assert rel_err(setup1d.from_elem_major(host(u), 4), ref[-1]) <= RTOL, scheme
+
+
+def test_golden_run_one_code_mlx(pkg, gpu):
+  """The executed reference run (One_code.mlx:106-140: N=2, K=20, T=2, uin=-sin(a^2 t)),
+  1341 steps on the GPU vs the oracle that reproduces the MATLAB outputs."""
+  S, mesh = mesh_pair(pkg, 2, 20)
+  u0 = np.sin(2 * np.pi * S["x"])
+  ref = oadv.advec1d(u0.copy(), 2.0, A, S, inflow="a2")
+  op = make_op(pkg, mesh, inflow="a2")
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  op.forward(u, 0.0, ref["dt"], ref["nsteps"])
+  assert rel_err(setup1d.from_elem_major(host(u), 3), ref["u"]) <= RTOL
+
+
+def test_ensemble_batch_matches_single_trajectories(pkg, gpu):
+  """batch trajectories in one plan == each trajectory alone (per-trajectory inflow/outflow)."""
+  import torch
+  S, mesh = mesh_pair(pkg, 4, 130)
+  rng = np.random.default_rng(11)
+  B = 3
+  u0s = [np.sin(2 * np.pi * rng.integers(1, 5) * S["x"] + rng.uniform(0, 6)) for _ in range(B)]
+  dt = oadv.bench_dt(S)
+  opb = make_op(pkg, mesh, batch=B)
+  ub = dev(np.concatenate([setup1d.to_elem_major(u) for u in u0s]), gpu)
+  opb.forward(ub, 0.0, dt, 6)
+  op1 = make_op(pkg, mesh)
+  for b in range(B):
+    u1 = dev(setup1d.to_elem_major(u0s[b]), gpu)
+    op1.forward(u1, 0.0, dt, 6)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(ub)[b * 650:(b + 1) * 650], host(u1))
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("scheme", ["lserk4", "euler"])
+@pytest.mark.parametrize("N,K", [(4, 50), (2, 300), (7, 260)])
+def test_adjoint_sweep_and_indicator(pkg, gpu, scheme, N, K):
+  rng = np.random.default_rng(N * 100 + K)
+  S, mesh = mesh_pair(pkg, N, K)
+  u0 = np.sin(2 * np.pi * S["x"]) + 0.3 * np.cos(6 * np.pi * S["x"])
+  dt = oadv.bench_dt(S) * (1.0 if scheme == "lserk4" else 0.1)
+  nsteps, src = 6, 0.7
+  snaps, times = oadv.forward_sweep(u0, 0.02, dt, nsteps, A, S, scheme=scheme)
+  g = rng.standard_normal(u0.shape)
+  op = make_op(pkg, mesh, time_scheme=scheme)
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  snap_d = op.new_field(nsteps + 1)
+  op.forward(u, 0.02, dt, nsteps, snap_d)
+  gsnaps = [setup1d.from_elem_major(host(snap_d[n]), N + 1) for n in range(nsteps + 1)]
+  for n in range(nsteps + 1):
+    assert rel_err(gsnaps[n], snaps[n]) <= RTOL
+  w_ref, eta_ref, _ = oadj.adjoint_sweep(g, gsnaps, times, dt, A, S, src_coef=src, scheme=scheme)
+  w = dev(setup1d.to_elem_major(g), gpu)
+  import torch
+  eta = torch.zeros(K, dtype=torch.float64, device=gpu)
+  op.adjoint(w, snap_d, 0.02, dt, nsteps, src_coef=src, eta=eta)
+  assert rel_err(setup1d.from_elem_major(host(w), N + 1), w_ref) <= RTOL
+  assert rel_err(host(eta), eta_ref) <= RTOL
+
+
+def test_adjoint_is_exact_transpose(pkg, gpu):
+  """<S u - S 0, w> == <u, S^T w> for one GPU step (dot-product test)."""
+  import torch
+  rng = np.random.default_rng(5)
+  S, mesh = mesh_pair(pkg, 4, 700)
+  op = make_op(pkg, mesh)
+  dt = oadv.bench_dt(S)
+  u = dev(rng.standard_normal(5 * 700), gpu)
+  z = torch.zeros_like(u)
+  su, s0 = u.clone(), z.clone()
+  snaps = op.new_field(2)
+  op.forward(su, 0.3, dt, 1, snaps)
+  op.forward(s0, 0.3, dt, 1)
+  w = dev(rng.standard_normal(5 * 700), gpu)
+  wt = w.clone()
+  op.adjoint(wt, snaps, 0.3, dt, 1)
+  lhs = float(torch.dot(su - s0, w))
+  rhs = float(torch.dot(u, wt))
+  assert abs(lhs - rhs) <= 1e-12 * abs(lhs)
+
+
+def test_adjoint_gradient_matches_finite_difference(pkg, gpu):
+  """dJ/du0 from the sweep vs a central difference of J (J is quadratic, so exact up to
+  rounding): the complex-step / FD method of matlab/test_jacobian.m:38-55."""
+  import torch
+  rng = np.random.default_rng(9)
+  N, K, nsteps, src = 3, 90, 5, 0.4
+  S, mesh = mesh_pair(pkg, N, K)
+  op = make_op(pkg, mesh)
+  dt = oadv.bench_dt(S)
+  g = dev(rng.standard_normal((N + 1) * K), gpu)
+  u0 = dev(rng.standard_normal((N + 1) * K), gpu)
+  d = dev(rng.standard_normal((N + 1) * K), gpu)
+
+  def J(u_init):
+    snaps = op.new_field(nsteps + 1)
+    op.forward(u_init.clone(), 0.0, dt, nsteps, snaps)
+    val = float(torch.dot(g, snaps[nsteps]))
+    for n in range(nsteps):
+      val += 0.5 * src * float(torch.dot(snaps[n], snaps[n]))
+    return val, snaps
+
+  _, snaps = J(u0)
+  w = g.clone()
+  op.adjoint(w, snaps, 0.0, dt, nsteps, src_coef=src)
+  h = 1e-3
+  fd = (J(u0 + h * d)[0] - J(u0 - h * d)[0]) / (2 * h)
+  ad = float(torch.dot(w, d))
+  assert abs(fd - ad) <= 1e-9 * abs(ad)
+
+
+# ---------------------------------------------------------------------------
+def _limiter_input(rng, S):
+  x = S["x"]
+  u = np.sin(2 * np.pi * x) + (x > 0.5) * 1.0 + 0.02 * rng.standard_normal(x.shape)
+  u[:, ::7] = u[:, ::7].mean(axis=0)  # some exactly-constant cells
+  return u
+
+
+@pytest.mark.parametrize("N", [1, 2, 4, 8])
+def test_slope_limiter_matches_SlopeLimitN(pkg, gpu, N):
+  import torch
+  rng = np.random.default_rng(N)
+  K = 517
+  S, mesh = mesh_pair(pkg, N, K)
+  u = _limiter_input(rng, S)
+  ref, ids_ref = olim.slope_limit_n(u, S, return_ids=True)
+  op = make_op(pkg, mesh)
+  ids = torch.zeros(K, dtype=torch.int32, device=gpu)
+  got = host(op.slope_limit(dev(setup1d.to_elem_major(u), gpu), ids=ids))
+  np.testing.assert_array_equal(np.nonzero(host(ids))[0], ids_ref)
+  assert 0 < ids_ref.size < K
+  np.testing.assert_allclose(setup1d.from_elem_major(got, N + 1), ref, rtol=0, atol=1e-13)
+
+
+# ---------------------------------------------------------------------------
+def test_argmax_numpy_semantics(pkg, gpu):
+  S, mesh = mesh_pair(pkg, 2, 4000)
+  op = make_op(pkg, mesh)
+  rng = np.random.default_rng(1)
+  cases = []
+  x = rng.standard_normal(12000)
+  cases.append(x)
+  y = x.copy()
+  y[[17, 9000, 11999]] = 50.0  # ties: first index wins
+  cases.append(y)
+  z = x.copy()
+  z[[3000, 4000]] = np.nan  # NaN is the maximum, first NaN wins
+  cases.append(z)
+  cases.append(-np.abs(x))
+  cases.append(np.zeros(5))
+  cases.append(np.array([-np.inf, -np.inf, -np.inf]))
+  for c in cases:
+    for use_abs in (False, True):
+      assert op.argmax(dev(c, gpu), use_abs=use_abs) == oadj.argmax(c, use_abs), (c[:4], use_abs)
+
+
+def test_sum_rows_fixed_order(pkg, gpu):
+  rng = np.random.default_rng(2)
+  x = rng.standard_normal((7, 3001)) * 10.0 ** rng.integers(-8, 8, (7, 3001))
+  got = host(pkg.operators.sum_rows(dev(x.ravel(), gpu), 7))
+  np.testing.assert_array_equal(got, oadj.sum_rows(x))
+
+
+def test_init_sine(pkg, gpu):
+  S, mesh = mesh_pair(pkg, 4, 333)
+  op = make_op(pkg, mesh, batch=2)
+  got = host(op.init_sine([0.7, 1.3], [3.0, 5.0], [0.1, 2.0]))
+  for b, (A_, m, ph) in enumerate([(0.7, 3.0, 0.1), (1.3, 5.0, 2.0)]):
+    ref = A_ * np.sin(2 * np.pi * m * S["x"] + ph)
+    np.testing.assert_allclose(setup1d.from_elem_major(got[b * 5 * 333:(b + 1) * 5 * 333], 5),
+                               ref, atol=1e-13)
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.slow
+def test_full_size_config2_forward_adjoint(pkg, gpu):
+  """BASELINE config 2 size (N=4, K=1,048,576): 2 fused steps vs the oracle, plus the
+  size-independent transpose identity of the adjoint at full size."""
+  import torch
+  N, K, nsteps = 4, 1 << 20, 2
+  S, mesh = mesh_pair(pkg, N, K)
+  u0 = np.sin(2 * np.pi * S["x"])
+  dt = oadv.bench_dt(S)
+  ref, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, A, S)
+  op = make_op(pkg, mesh)
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  snaps = op.new_field(nsteps + 1)
+  op.forward(u, 0.0, dt, nsteps, snaps)
+  assert rel_err(setup1d.from_elem_major(host(u), N + 1), ref[-1]) <= RTOL
+  rng = np.random.default_rng(0)
+  g = rng.standard_normal(u0.shape)
+  gsnaps = [setup1d.from_elem_major(host(snaps[n]), N + 1) for n in range(nsteps + 1)]
+  w_ref, eta_ref, _ = oadj.adjoint_sweep(g, gsnaps, times, dt, A, S)
+  w = dev(setup1d.to_elem_major(g), gpu)
+  eta = torch.zeros(K, dtype=torch.float64, device=gpu)
+  op.adjoint(w, snaps, 0.0, dt, nsteps, eta=eta)
+  assert rel_err(setup1d.from_elem_major(host(w), N + 1), w_ref) <= RTOL
+  assert rel_err(host(eta), eta_ref) <= RTOL
+  assert op.argmax(eta) == int(np.argmax(np.abs(host(eta))))
