@@ -15,6 +15,7 @@ HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "include", "dg_advec.h"
 DG_OK, DG_ERR_ARG, DG_ERR_HIP, DG_ERR_NOMEM = 0, -1, -2, -3
 DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T = 0, 1
 DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
+DG_TUNE_ELEMS_PER_LANE = 1
 
 _c_dbl_p = ctypes.POINTER(ctypes.c_double)
 _vp = ctypes.c_void_p
@@ -29,6 +30,7 @@ SIGNATURES = {
                               _c_dbl_p, ctypes.c_double, _i32, _i32, ctypes.POINTER(_vp)]),
     "dg_plan_destroy": (_i32, [_vp]),
     "dg_plan_query": (_i32, [_vp, ctypes.POINTER(_i64)]),
+    "dg_plan_tune": (_i32, [_vp, _i32, _i64]),
     "dg_advec_rhs": (_i32, [_vp, _vp, _vp, ctypes.c_double, _vp]),
     "dg_lserk4_fwd": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp]),
     "dg_lserk4_adj": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32,

@@ -34,7 +34,9 @@ def build(force=False, verbose=True, extra_flags=()):
          "-I", INCLUDE, *extra_flags, "-o", tmp, SRC]
   if verbose:
     print("[build_ext]", " ".join(cmd))
-  subprocess.run(cmd, check=True)
+  r = subprocess.run(cmd)
+  if r.returncode != 0:
+    raise RuntimeError(f"hipcc failed ({r.returncode}); {OUT} was NOT updated")
   os.replace(tmp, OUT)
   return OUT
 

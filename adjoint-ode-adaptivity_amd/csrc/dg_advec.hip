@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <utility>
@@ -92,8 +93,24 @@ template <int NP> struct OpArgs {
   double L1[NP];
 };
 
+// The same operator in even/odd node coordinates.  LGL nodes are symmetric about 0, so
+// with J the node-reversal matrix J*Dr*J = -Dr and LIFT(:,2) = J*LIFT(:,1).  Per element
+//   e_k = (u_k + u_{N-k})/2,  o_k = (u_k - u_{N-k})/2   (k < NO),   e_NO = u_mid (Np odd)
+// and the element operator splits into an odd->even and an even->odd block:
+//   rhs_e = Qeo o + le*(du0 - du1),   rhs_o = Qoe e + lo*(du0 + du1)
+// which is 2*NE*NO + NP fused multiply-adds per stage instead of NP*NP + 2*NP.
+// The blocks are built and checked on the host (make_eo).
+template <int NP> struct EOArgs {
+  static constexpr int NE = (NP + 1) / 2;
+  static constexpr int NO = NP / 2;
+  double Qeo[NE * NO];  // rhs_e[k] += Qeo[k*NO + j] * o[j]
+  double Qoe[NO * NE];  // rhs_o[k] += Qoe[k*NE + j] * e[j]
+  double le[NE];
+  double lo[NO];
+};
+
 template <int NP, int NS> struct StepArgs {
-  OpArgs<NP> op;
+  EOArgs<NP> op;
   double sc;          // dt * s (uniform mesh) or dt (non-uniform: times scale[k])
   double uin[NS];     // inflow value at each stage time
   int64_t ktot;       // batch * K elements
@@ -101,7 +118,7 @@ template <int NP, int NS> struct StepArgs {
 };
 
 template <int NP> struct AdjArgs {
-  OpArgs<NP> op;
+  EOArgs<NP> op;
   double sc;          // as StepArgs
   double uin_res;     // inflow value at t_{n+1} for the residual
   double src;         // functional source coefficient for node n+1
@@ -137,6 +154,68 @@ __device__ __forceinline__ int load_tile(const double* __restrict__ g, int64_t e
   return off;
 }
 
+
+// ---------------------------------------------------------------------------
+// Tile geometry of the fused step kernels.  A workgroup of kBlock lanes owns a tile of
+// T = kBlock*EPL consecutive elements; lane l holds elements l, l+kBlock, ... (EPL of
+// them) in VGPRs.  The dependency cone of one step is NS elements per side, so the
+// TE = T - 2*NS interior elements are exact and written back.  EPL > 1 puts more bytes
+// in flight per resident wave (the kernels are co-limited by HBM and fp64 VALU, and one
+// 256-element tile per workgroup does not hold enough loads in flight to cover HBM
+// latency at the residency their 106 SGPRs allow).
+// ---------------------------------------------------------------------------
+template <int NP, int EPL> struct TileGeo {
+  static constexpr int T = kBlock * EPL;
+  static constexpr int kVec = (T * NP + 2 + 2 * kBlock - 1) / (2 * kBlock);  // double2 / lane
+  static constexpr int kTileD = T * NP + 2;  // staging image (+2: 16-byte realignment)
+  static constexpr int kFaceD = 4 * (T + 2);  // 2 double-buffered face arrays, padded by 1
+  static constexpr int kLds = kTileD > kFaceD ? kTileD : kFaceD;
+};
+
+// Issue the 16-byte loads of one tile image into registers (coalesced: lane-consecutive
+// double2), then commit them to LDS.  Elements outside [0, ktot) read as zero.
+template <int NP, int EPL> struct TileRegs {
+  double2 v[TileGeo<NP, EPL>::kVec];
+  int off;
+};
+
+template <int NP, int EPL>
+__device__ __forceinline__ void tile_issue(const double* __restrict__ g, int64_t e0, int64_t nd,
+                                           TileRegs<NP, EPL>& r) {
+  using G = TileGeo<NP, EPL>;
+  const int64_t d0 = e0 * NP;
+  const int64_t base = d0 & ~int64_t(1);
+  r.off = int(d0 - base);
+  const int nvec = (G::T * NP + r.off + 1) >> 1;
+  const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = threadIdx.x + q * kBlock;
+    const int64_t gd = base + 2 * int64_t(v);
+    double2 val = make_double2(0.0, 0.0);
+    if (v < nvec) {
+      if (gd >= 0 && gd + 1 < nd) {
+        val = g2[gd >> 1];
+      } else {
+        if (gd >= 0 && gd < nd) val.x = g[gd];
+        if (gd + 1 >= 0 && gd + 1 < nd) val.y = g[gd + 1];
+      }
+    }
+    r.v[q] = val;
+  }
+}
+
+template <int NP, int EPL>
+__device__ __forceinline__ void tile_commit(const TileRegs<NP, EPL>& r, double* __restrict__ lds) {
+  using G = TileGeo<NP, EPL>;
+  const int nvec = (G::T * NP + r.off + 1) >> 1;
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = threadIdx.x + q * kBlock;
+    if (v < nvec) *reinterpret_cast<double2*>(&lds[2 * v]) = r.v[q];
+  }
+}
+
 // Store `count` doubles from lds[0..count) to g[o0..o0+count); o0 must be even.
 __device__ __forceinline__ void store_run(double* __restrict__ g, int64_t o0, int64_t count,
                                           const double* __restrict__ lds) {
@@ -152,201 +231,331 @@ __device__ __forceinline__ void store_run(double* __restrict__ g, int64_t o0, in
   }
 }
 
+// Per-element geometry: global element e = e0 + el, position kl inside its trajectory.
+struct Elem {
+  int64_t e;
+  int32_t kl;
+  bool inrange, first, last, valid;
+};
+
+template <int H, int T>
+__device__ __forceinline__ Elem elem_info(int64_t e0, int el, int64_t ktot, int32_t K) {
+  Elem E;
+  E.e = e0 + el;
+  E.inrange = (E.e >= 0 && E.e < ktot);
+  // ktot < 2^31 (checked at plan creation): 32-bit division.
+  E.kl = E.inrange ? int32_t(uint32_t(E.e) % uint32_t(K)) : 0;
+  E.first = (E.kl == 0);
+  E.last = (E.kl == K - 1);
+  E.valid = E.inrange && el >= H && el < T - H;
+  return E;
+}
+
 // ---------------------------------------------------------------------------
-// Forward fused step.
+// Forward fused step: all NS stages of AdvecRHS1D + the low-storage update for the EPL
+// elements of each lane.  UNI: the operator constants already carry dt*2/h.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI>
+template <int NP, int NS, bool UNI, int EPL>
 __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
                                                  double* __restrict__ uout,
                                                  double* __restrict__ uout2,
                                                  const double* __restrict__ scale,
                                                  StepArgs<NP, NS> args) {
-  constexpr int H = NS;               // dependency cone grows one element per stage
-  constexpr int TE = kBlock - 2 * H;  // output elements per tile (even)
+  using G = TileGeo<NP, EPL>;
+  constexpr int T = G::T;
+  constexpr int H = NS;          // dependency cone grows one element per stage
+  constexpr int TE = T - 2 * H;  // output elements per tile (even)
   static_assert(TE % 2 == 0, "tile output must be 16-byte aligned");
-  __shared__ __attribute__((aligned(16))) double tile[kBlock * NP + 2];
-  __shared__ double faceL[2][kBlock];
-  __shared__ double faceR[2][kBlock];
-
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int lane = threadIdx.x;
-  const int64_t tile_id = blockIdx.x;
-  const int64_t e0 = tile_id * TE - H;
-  const int64_t e = e0 + lane;
+  const int64_t tile = blockIdx.x;
+  const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
-  const int off = load_tile<NP>(uin, e0, nd, tile);
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  TileRegs<NP, EPL> pf;
+  tile_issue<NP, EPL>(uin, e0, nd, pf);
+  tile_commit<NP, EPL>(pf, lds);
   __syncthreads();
-
-  double u[NP];
+  double ev[EPL][NE], od[EPL][NO];  // the element state in even/odd coordinates
+  Elem E[EPL];
+  double sc[EPL];
 #pragma unroll
-  for (int i = 0; i < NP; ++i) u[i] = tile[off + lane * NP + i];
+  for (int m = 0; m < EPL; ++m) {
+    const int el = m * kBlock + lane;
+    double u[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) u[i] = lds[pf.off + el * NP + i];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      ev[m][k] = 0.5 * (u[k] + u[N - k]);
+      od[m][k] = 0.5 * (u[k] - u[N - k]);
+    }
+    if constexpr (NE > NO) ev[m][NO] = u[NO];
+    E[m] = elem_info<H, T>(e0, el, args.ktot, args.K);
+    sc[m] = args.sc;
+    if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
+  }
+  __syncthreads();  // the face arrays below alias the staging image
 
-  const bool inrange = (e >= 0 && e < args.ktot);
-  const int32_t kl = inrange ? int32_t(e % args.K) : 0;
-  const bool first = (kl == 0);
-  const bool last = (kl == args.K - 1);
-  double sc = args.sc;
-  if constexpr (!UNI) sc *= inrange ? scale[kl] : 0.0;
-
-  double res[NP];
+  double re[EPL][NE], ro[EPL][NO];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const int b = s & 1;
-    faceL[b][lane] = u[0];
-    faceR[b][lane] = u[NP - 1];
-    __syncthreads();
-    double uL = (lane > 0) ? faceR[b][lane - 1] : u[0];
-    const double uR = (lane < kBlock - 1) ? faceL[b][lane + 1] : u[NP - 1];
-    if (first) uL = args.uin[s];
-    const double du0 = u[0] - uL;
-    const double du1 = last ? 0.0 : (u[NP - 1] - uR);
-    double acc[NP];
+    const int fL = (s & 1) * 2 * (T + 2);  // faceL = lds[fL ...], faceR = lds[fR ...]
+    const int fR = fL + (T + 2);
+    double u0[EPL], uN[EPL];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      double t = args.op.L0[i] * du0;
-      t = fma(args.op.L1[i], du1, t);
-#pragma unroll
-      for (int j = 0; j < NP; ++j) t = fma(args.op.Dm[i * NP + j], u[j], t);
-      acc[i] = t;
+    for (int m = 0; m < EPL; ++m) {
+      const int el = m * kBlock + lane;
+      u0[m] = ev[m][0] + od[m][0];
+      uN[m] = ev[m][0] - od[m][0];
+      lds[fL + el + 1] = u0[m];
+      lds[fR + el + 1] = uN[m];
     }
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      if (s == 0) {
-        res[i] = sc * acc[i];  // rk4a(1) = 0: the residual register is step-local
-      } else {
-        res[i] = fma(RK<NS>::A(s), res[i], sc * acc[i]);
+    for (int m = 0; m < EPL; ++m) {
+      const int el = m * kBlock + lane;
+      // faceR[el] is element el-1's right node, faceL[el+2] element el+1's left node; the
+      // pad entries are only read by the outermost halo elements, whose results are dropped.
+      const double uL = E[m].first ? args.uin[s] : lds[fR + el];
+      const double uR = lds[fL + el + 2];
+      const double du0 = u0[m] - uL;
+      const double du1 = E[m].last ? 0.0 : (uN[m] - uR);
+      const double dlt = du0 - du1, sig = du0 + du1;
+      double ae[NE], ao[NO];
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        double t = args.op.le[k] * dlt;
+#pragma unroll
+        for (int j = 0; j < NO; ++j) t = fma(args.op.Qeo[k * NO + j], od[m][j], t);
+        ae[k] = UNI ? t : sc[m] * t;
       }
-      u[i] = fma(RK<NS>::B(s), res[i], u[i]);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        double t = args.op.lo[k] * sig;
+#pragma unroll
+        for (int j = 0; j < NE; ++j) t = fma(args.op.Qoe[k * NE + j], ev[m][j], t);
+        ao[k] = UNI ? t : sc[m] * t;
+      }
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        re[m][k] = (s == 0) ? ae[k] : fma(RK<NS>::A(s), re[m][k], ae[k]);  // rk4a(1) = 0
+        ev[m][k] = fma(RK<NS>::B(s), re[m][k], ev[m][k]);
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        ro[m][k] = (s == 0) ? ao[k] : fma(RK<NS>::A(s), ro[m][k], ao[k]);
+        od[m][k] = fma(RK<NS>::B(s), ro[m][k], od[m][k]);
+      }
     }
   }
 
-  // Stage the TE valid elements back through LDS (all reads of `tile` happened before
-  // the first stage barrier) and store them with 16-byte coalesced writes.
-  if (lane >= H && lane < kBlock - H) {
+  __syncthreads();  // the last stage's face reads are done before the image is rewritten
 #pragma unroll
-    for (int i = 0; i < NP; ++i) tile[(lane - H) * NP + i] = u[i];
+  for (int m = 0; m < EPL; ++m) {
+    const int el = m * kBlock + lane;
+    if (el >= H && el < T - H) {
+      double* o = lds + (el - H) * NP;
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        o[k] = ev[m][k] + od[m][k];
+        o[N - k] = ev[m][k] - od[m][k];
+      }
+      if constexpr (NE > NO) o[NO] = ev[m][NO];
+    }
   }
   __syncthreads();
-  const int64_t o0 = tile_id * TE * NP;
+  const int64_t o0 = tile * TE * NP;
   const int64_t rem = nd - o0;
   const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
-  store_run(uout, o0, count, tile);
-  if (uout2 != nullptr) store_run(uout2, o0, count, tile);
+  store_run(uout, o0, count, lds);
+  if (uout2 != nullptr) store_run(uout2, o0, count, lds);
 }
 
 // ---------------------------------------------------------------------------
-// Adjoint fused step: w^n = S^T (w^{n+1} + src*u^{n+1}), eta += DWR contribution.
+// Adjoint fused step: w^n = S^T (w^{n+1} + src*u^{n+1}) and the DWR contribution.
 // Reverse of stage s (forward: r = A_s r + dt L u ; u = u + B_s r):
 //   lr += B_s lu ;  lu += dt L^T lr ;  lr = A_s lr
 // L^T per element with q = sc*lr, g0 = L0.q, g1 = L1.q:
 //   (L^T)_j = sum_i Dm[i][j] q_i + [j=0](g0 - g1_{left}) + [j=N]([!last] g1 - [!last] g0_{right})
+// Indicator: eta += dt * sum_i w_i * s*(L0_i du0 + L1_i du1) = sc*(du0*(L0.w) + du1*(L1.w)).
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI>
+template <int NP, int NS, bool UNI, int EPL>
 __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
                                                 double* __restrict__ wout,
                                                 const double* __restrict__ usnap,
                                                 double* __restrict__ eta,
                                                 const double* __restrict__ scale,
                                                 AdjArgs<NP> args) {
+  using G = TileGeo<NP, EPL>;
+  constexpr int T = G::T;
   constexpr int H = NS;
-  constexpr int TE = kBlock - 2 * H;
-  __shared__ __attribute__((aligned(16))) double tile_w[kBlock * NP + 2];
-  __shared__ __attribute__((aligned(16))) double tile_u[kBlock * NP + 2];
-  __shared__ double G0[2][kBlock];
-  __shared__ double G1[2][kBlock];
-
+  constexpr int TE = T - 2 * H;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int lane = threadIdx.x;
-  const int64_t tile_id = blockIdx.x;
-  const int64_t e0 = tile_id * TE - H;
-  const int64_t e = e0 + lane;
+  const int64_t tile = blockIdx.x;
+  const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
-  const int offw = load_tile<NP>(win, e0, nd, tile_w);
-  const int offu = load_tile<NP>(usnap, e0, nd, tile_u);
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  TileRegs<NP, EPL> pw, pu;
+  tile_issue<NP, EPL>(win, e0, nd, pw);
+  tile_issue<NP, EPL>(usnap, e0, nd, pu);
+  // The adjoint lives in the dual even/odd coordinates (the transpose of the inverse
+  // transform): we_k = w_k + w_{N-k}, wo_k = w_k - w_{N-k}, we_NO = w_mid; back with
+  // w_k = (we_k + wo_k)/2, w_{N-k} = (we_k - wo_k)/2.  The adjoint tile is staged and read
+  // out first, then the snapshot tile, through one LDS image; the face arrays of the
+  // stages alias it afterwards.
+  tile_commit<NP, EPL>(pw, lds);
+  __syncthreads();
+  double we[EPL][NE], wo[EPL][NO];
+#pragma unroll
+  for (int m = 0; m < EPL; ++m) {
+    const int el = m * kBlock + lane;
+    double w[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) w[i] = lds[pw.off + el * NP + i];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      we[m][k] = w[k] + w[N - k];
+      wo[m][k] = w[k] - w[N - k];
+    }
+    if constexpr (NE > NO) we[m][NO] = w[NO];
+  }
+  __syncthreads();
+  tile_commit<NP, EPL>(pu, lds);
   __syncthreads();
 
-  const bool inrange = (e >= 0 && e < args.ktot);
-  const int32_t kl = inrange ? int32_t(e % args.K) : 0;
-  const bool first = (kl == 0);
-  const bool last = (kl == args.K - 1);
-  double sc = args.sc;
-  if constexpr (!UNI) sc *= inrange ? scale[kl] : 0.0;
-
-  double lu[NP], us[NP];
+  Elem E[EPL];
+  double sc[EPL];
+  double contrib[EPL];
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    lu[i] = tile_w[offw + lane * NP + i];
-    us[i] = tile_u[offu + lane * NP + i];
-  }
-  // Neighbour face values of the snapshot for the jump residual.
-  const double usL = (lane > 0) ? tile_u[offu + (lane - 1) * NP + (NP - 1)] : us[0];
-  const double usR = (lane < kBlock - 1) ? tile_u[offu + (lane + 1) * NP] : us[NP - 1];
-
-  // Functional source K^{n+1} = src * u^{n+1}.
-  if (args.src != 0.0) {
+  for (int m = 0; m < EPL; ++m) {
+    const int el = m * kBlock + lane;
+    E[m] = elem_info<H, T>(e0, el, args.ktot, args.K);
+    sc[m] = args.sc;
+    if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
+    const int off = pu.off;
+    const double* us = lds + off + el * NP;
+    if (args.src != 0.0) {  // functional source K^{n+1} = src * u^{n+1} (dual coordinates)
 #pragma unroll
-    for (int i = 0; i < NP; ++i) lu[i] = fma(args.src, us[i], lu[i]);
-  }
-
-  // Dual-weighted interelement-jump residual at t_{n+1}:
-  //   dt * sum_i w_i * s*(L0_i du0 + L1_i du1) = sc * (du0 * (L0.w) + du1 * (L1.w))
-  if (args.has_eta) {
-    const double du0 = us[0] - (first ? args.uin_res : usL);
-    const double du1 = last ? 0.0 : (us[NP - 1] - usR);
-    double gw0 = 0.0, gw1 = 0.0;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      gw0 = fma(args.op.L0[i], lu[i], gw0);
-      gw1 = fma(args.op.L1[i], lu[i], gw1);
+      for (int k = 0; k < NO; ++k) {
+        we[m][k] = fma(args.src, us[k] + us[N - k], we[m][k]);
+        wo[m][k] = fma(args.src, us[k] - us[N - k], wo[m][k]);
+      }
+      if constexpr (NE > NO) we[m][NO] = fma(args.src, us[NO], we[m][NO]);
     }
-    const double contrib = sc * fma(du0, gw0, du1 * gw1);
-    if (inrange && lane >= H && lane < kBlock - H) eta[e] += contrib;
-  }
-
-  double lr[NP];
+    contrib[m] = 0.0;
+    if (args.has_eta) {
+      // Neighbour face values of the snapshot for the jump residual.
+      const double usL = (el > 0) ? lds[off + (el - 1) * NP + (NP - 1)] : us[0];
+      const double usR = (el < T - 1) ? lds[off + (el + 1) * NP] : us[NP - 1];
+      const double du0 = us[0] - (E[m].first ? args.uin_res : usL);
+      const double du1 = E[m].last ? 0.0 : (us[NP - 1] - usR);
+      // L0.w = le.we + lo.wo and L1.w = -le.we + lo.wo
+      double pe = 0.0, po = 0.0;
 #pragma unroll
-  for (int i = 0; i < NP; ++i) lr[i] = 0.0;
+      for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[m][k], pe);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[m][k], po);
+      contrib[m] = fma(du0 - du1, pe, (du0 + du1) * po);
+      if constexpr (!UNI) contrib[m] *= sc[m];
+    }
+  }
+  __syncthreads();  // the face arrays below alias the staging image
+
+  double le_[EPL][NE], lo_[EPL][NO];  // the stage residual's adjoint
+#pragma unroll
+  for (int m = 0; m < EPL; ++m) {
+#pragma unroll
+    for (int k = 0; k < NE; ++k) le_[m][k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) lo_[m][k] = 0.0;
+  }
 
 #pragma unroll
   for (int ss = 0; ss < NS; ++ss) {
     const int s = NS - 1 - ss;
-    const int b = ss & 1;
-    double q[NP];
-    double g0 = 0.0, g1 = 0.0;
+    const int f0 = (ss & 1) * 2 * (T + 2);  // g0 = lds[f0 ...], g1 = lds[f1 ...]
+    const int f1 = f0 + (T + 2);
+    double qe[EPL][NE], qo[EPL][NO];
+    double g0[EPL], g1[EPL];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      lr[i] = fma(RK<NS>::B(s), lu[i], lr[i]);
-      q[i] = sc * lr[i];
-      g0 = fma(args.op.L0[i], q[i], g0);
-      g1 = fma(args.op.L1[i], q[i], g1);
+    for (int m = 0; m < EPL; ++m) {
+      const int el = m * kBlock + lane;
+      double gd = 0.0, gs = 0.0;
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        le_[m][k] = fma(RK<NS>::B(s), we[m][k], le_[m][k]);
+        qe[m][k] = UNI ? le_[m][k] : sc[m] * le_[m][k];
+        gd = fma(args.op.le[k], qe[m][k], gd);
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        lo_[m][k] = fma(RK<NS>::B(s), wo[m][k], lo_[m][k]);
+        qo[m][k] = UNI ? lo_[m][k] : sc[m] * lo_[m][k];
+        gs = fma(args.op.lo[k], qo[m][k], gs);
+      }
+      // adjoints of du0 and du1 (du0 - du1 feeds the even part, du0 + du1 the odd part)
+      g0[m] = gd + gs;
+      g1[m] = E[m].last ? 0.0 : (gs - gd);
+      lds[f0 + el + 1] = g0[m];
+      lds[f1 + el + 1] = g1[m];
     }
-    G0[b][lane] = g0;
-    G1[b][lane] = g1;
     __syncthreads();
-    const double g1_left = (!first && lane > 0) ? G1[b][lane - 1] : 0.0;
-    const double g0_right = (!last && lane < kBlock - 1) ? G0[b][lane + 1] : 0.0;
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      double t = lu[j];
+    for (int m = 0; m < EPL; ++m) {
+      const int el = m * kBlock + lane;
+      // du0 = u_0 - (left neighbour's u_N); du1 = u_N - (right neighbour's u_0), with
+      // u_0 = e_0 + o_0 and u_N = e_0 - o_0.
+      const double gl = E[m].first ? 0.0 : lds[f1 + el];      // g1 of element k-1
+      const double gr = E[m].last ? 0.0 : lds[f0 + el + 2];   // g0 of element k+1
 #pragma unroll
-      for (int i = 0; i < NP; ++i) t = fma(args.op.Dm[i * NP + j], q[i], t);
-      lu[j] = t;
+      for (int j = 0; j < NE; ++j) {
+        double t = we[m][j];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[m][k], t);
+        we[m][j] = t;
+      }
+#pragma unroll
+      for (int j = 0; j < NO; ++j) {
+        double t = wo[m][j];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[m][k], t);
+        wo[m][j] = t;
+      }
+      we[m][0] += (g0[m] + g1[m]) - (gr + gl);
+      wo[m][0] += (g0[m] - g1[m]) + (gr - gl);
+#pragma unroll
+      for (int k = 0; k < NE; ++k) le_[m][k] = RK<NS>::A(s) * le_[m][k];
+#pragma unroll
+      for (int k = 0; k < NO; ++k) lo_[m][k] = RK<NS>::A(s) * lo_[m][k];
     }
-    lu[0] += g0 - g1_left;
-    lu[NP - 1] += (last ? 0.0 : g1) - g0_right;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) lr[i] = RK<NS>::A(s) * lr[i];
   }
 
-  if (lane >= H && lane < kBlock - H) {
 #pragma unroll
-    for (int i = 0; i < NP; ++i) tile_w[(lane - H) * NP + i] = lu[i];
+  for (int m = 0; m < EPL; ++m)
+    if (args.has_eta && E[m].valid) eta[E[m].e] += contrib[m];
+  __syncthreads();  // the last stage's face reads are done before the image is rewritten
+#pragma unroll
+  for (int m = 0; m < EPL; ++m) {
+    const int el = m * kBlock + lane;
+    if (el >= H && el < T - H) {
+      double* o = lds + (el - H) * NP;
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        o[k] = 0.5 * (we[m][k] + wo[m][k]);
+        o[N - k] = 0.5 * (we[m][k] - wo[m][k]);
+      }
+      if constexpr (NE > NO) o[NO] = we[m][NO];
+    }
   }
   __syncthreads();
-  const int64_t o0 = tile_id * TE * NP;
+  const int64_t o0 = tile * TE * NP;
   const int64_t rem = nd - o0;
   const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
-  store_run(wout, o0, count, tile_w);
+  store_run(wout, o0, count, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -617,6 +826,8 @@ struct dg_plan {
   double* d_scratch = nullptr;
   double* d_pv = nullptr;
   int64_t* d_pi = nullptr;
+  // tuning (dg_plan_tune): elements per lane of the step kernels (tile = 256*epl elements)
+  int epl = 1;
 };
 
 namespace {
@@ -625,14 +836,75 @@ double inflow_value(const dg_plan* p, double t) {
   return (p->inflow == DG_INFLOW_SIN_A2T) ? -std::sin(p->a * p->a * t) : -std::sin(p->a * t);
 }
 
-template <int NP> OpArgs<NP> make_op(const dg_plan* p) {
+// scale = 1 gives the plain operator (rhs); the steppers fold dt*2/h into it on uniform meshes.
+template <int NP> OpArgs<NP> make_op(const dg_plan* p, double scale = 1.0) {
   OpArgs<NP> op;
   for (int i = 0; i < NP; ++i) {
-    for (int j = 0; j < NP; ++j) op.Dm[i * NP + j] = -p->a * p->Dr[i * NP + j];
-    op.L0[i] = (-p->a / 2.0) * p->LIFT[i * 2 + 0];
-    op.L1[i] = (p->a / 2.0) * p->LIFT[i * 2 + 1];
+    for (int j = 0; j < NP; ++j) op.Dm[i * NP + j] = scale * (-p->a * p->Dr[i * NP + j]);
+    op.L0[i] = scale * ((-p->a / 2.0) * p->LIFT[i * 2 + 0]);
+    op.L1[i] = scale * ((p->a / 2.0) * p->LIFT[i * 2 + 1]);
   }
   return op;
+}
+
+// Even/odd blocks of the element operator (see EOArgs).  Returns false if the operator
+// is not centro-(anti)symmetric to 1e-12, i.e. the nodes are not symmetric.
+template <int NP> bool make_eo(const dg_plan* p, double scale, EOArgs<NP>* out) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  double Dm[NP][NP], L0[NP], L1[NP], T[NP][NP] = {}, Ti[NP][NP] = {};
+  for (int i = 0; i < NP; ++i) {
+    for (int j = 0; j < NP; ++j) Dm[i][j] = scale * (-p->a * p->Dr[i * NP + j]);
+    L0[i] = scale * ((-p->a / 2.0) * p->LIFT[i * 2 + 0]);
+    L1[i] = scale * ((p->a / 2.0) * p->LIFT[i * 2 + 1]);
+  }
+  for (int k = 0; k < NO; ++k) {  // rows: e_0..e_{NE-1}, o_0..o_{NO-1}
+    T[k][k] += 0.5; T[k][N - k] += 0.5;
+    T[NE + k][k] += 0.5; T[NE + k][N - k] -= 0.5;
+    Ti[k][k] += 1.0; Ti[k][NE + k] += 1.0;
+    Ti[N - k][k] += 1.0; Ti[N - k][NE + k] -= 1.0;
+  }
+  if (NE > NO) { T[NO][NO] = 1.0; Ti[NO][NO] = 1.0; }
+  double TD[NP][NP], Q[NP][NP], l0[NP], l1[NP];
+  for (int i = 0; i < NP; ++i)
+    for (int j = 0; j < NP; ++j) {
+      double t = 0.0;
+      for (int k = 0; k < NP; ++k) t += T[i][k] * Dm[k][j];
+      TD[i][j] = t;
+    }
+  double qmax = 0.0, lmax = 0.0;
+  for (int i = 0; i < NP; ++i) {
+    for (int j = 0; j < NP; ++j) {
+      double t = 0.0;
+      for (int k = 0; k < NP; ++k) t += TD[i][k] * Ti[k][j];
+      Q[i][j] = t;
+      qmax = std::fmax(qmax, std::fabs(t));
+    }
+    double a0 = 0.0, a1 = 0.0;
+    for (int k = 0; k < NP; ++k) {
+      a0 += T[i][k] * L0[k];
+      a1 += T[i][k] * L1[k];
+    }
+    l0[i] = a0;
+    l1[i] = a1;
+    lmax = std::fmax(lmax, std::fmax(std::fabs(a0), std::fabs(a1)));
+  }
+  bool ok = true;
+  const double tq = 1e-12 * qmax, tl = 1e-12 * lmax;
+  for (int i = 0; i < NE; ++i)
+    for (int j = 0; j < NE; ++j) ok = ok && std::fabs(Q[i][j]) <= tq;           // even->even
+  for (int i = 0; i < NO; ++i)
+    for (int j = 0; j < NO; ++j) ok = ok && std::fabs(Q[NE + i][NE + j]) <= tq;  // odd->odd
+  for (int k = 0; k < NE; ++k) ok = ok && std::fabs(l0[k] + l1[k]) <= tl;
+  for (int k = 0; k < NO; ++k) ok = ok && std::fabs(l0[NE + k] - l1[NE + k]) <= tl;
+  if (out) {
+    for (int k = 0; k < NE; ++k)
+      for (int j = 0; j < NO; ++j) out->Qeo[k * NO + j] = Q[k][NE + j];
+    for (int k = 0; k < NO; ++k)
+      for (int j = 0; j < NE; ++j) out->Qoe[k * NE + j] = Q[NE + k][j];
+    for (int k = 0; k < NE; ++k) out->le[k] = 0.5 * (l0[k] - l1[k]);
+    for (int k = 0; k < NO; ++k) out->lo[k] = 0.5 * (l0[NE + k] + l1[NE + k]);
+  }
+  return ok;
 }
 
 template <int NP> LimArgs<NP> make_lim(const dg_plan* p) {
@@ -652,46 +924,75 @@ template <int NP> LimArgs<NP> make_lim(const dg_plan* p) {
 
 inline unsigned grid_for(int64_t n, int64_t per) { return unsigned((n + per - 1) / per); }
 
-template <int NP, int NS>
-int launch_step_t(const dg_plan* p, const double* in, double* out, double* out2,
-                  double t, double dt, hipStream_t st) {
+template <int NP, int NS, int EPL>
+int launch_step_e(const dg_plan* p, const double* in, double* out, double* out2, double t,
+                  double dt, hipStream_t st) {
   StepArgs<NP, NS> a;
-  a.op = make_op<NP>(p);
-  a.sc = p->uniform ? dt * p->s_uniform : dt;
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  a.sc = dt;  // non-uniform meshes multiply by scale[k] in the kernel
   for (int s = 0; s < NS; ++s) a.uin[s] = inflow_value(p, t + RK<NS>::C(s) * dt);
   a.ktot = p->ktot;
   a.K = int32_t(p->K);
-  const unsigned grid = grid_for(p->ktot, kBlock - 2 * NS);
+  constexpr int TE = kBlock * EPL - 2 * NS;
+  const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_step<NP, NS, true>), dim3(grid), dim3(kBlock), 0, st, in, out, out2,
-                       p->d_scale, a);
+    hipLaunchKernelGGL((k_step<NP, NS, true, EPL>), dim3(grid), dim3(kBlock), 0, st, in, out,
+                       out2, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_step<NP, NS, false>), dim3(grid), dim3(kBlock), 0, st, in, out, out2,
-                       p->d_scale, a);
+    hipLaunchKernelGGL((k_step<NP, NS, false, EPL>), dim3(grid), dim3(kBlock), 0, st, in, out,
+                       out2, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-template <int NP, int NS>
-int launch_adj_t(const dg_plan* p, const double* win, double* wout, const double* usnap,
+template <int NP, int NS, int EPL>
+int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double* usnap,
                  double* eta, double t_next, double dt, double src, hipStream_t st) {
   AdjArgs<NP> a;
-  a.op = make_op<NP>(p);
-  a.sc = p->uniform ? dt * p->s_uniform : dt;
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  a.sc = dt;
   a.uin_res = inflow_value(p, t_next);
   a.src = src;
   a.ktot = p->ktot;
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr;
-  const unsigned grid = grid_for(p->ktot, kBlock - 2 * NS);
+  constexpr int TE = kBlock * EPL - 2 * NS;
+  const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_adj<NP, NS, true>), dim3(grid), dim3(kBlock), 0, st, win, wout, usnap,
-                       eta, p->d_scale, a);
+    hipLaunchKernelGGL((k_adj<NP, NS, true, EPL>), dim3(grid), dim3(kBlock), 0, st, win, wout,
+                       usnap, eta, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_adj<NP, NS, false>), dim3(grid), dim3(kBlock), 0, st, win, wout,
+    hipLaunchKernelGGL((k_adj<NP, NS, false, EPL>), dim3(grid), dim3(kBlock), 0, st, win, wout,
                        usnap, eta, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
+}
+
+template <int NP, int NS>
+int launch_step_t(const dg_plan* p, const double* in, double* out, double* out2, double t,
+                  double dt, hipStream_t st) {
+  // 4 elements per lane is instantiated for Np <= 5 only (register budget; larger Np
+  // use 2).
+  switch (p->epl) {
+    case 1: return launch_step_e<NP, NS, 1>(p, in, out, out2, t, dt, st);
+    case 4:
+      if constexpr (NP <= 5) return launch_step_e<NP, NS, 4>(p, in, out, out2, t, dt, st);
+      [[fallthrough]];
+    default: return launch_step_e<NP, NS, 2>(p, in, out, out2, t, dt, st);
+  }
+}
+
+template <int NP, int NS>
+int launch_adj_t(const dg_plan* p, const double* win, double* wout, const double* usnap,
+                 double* eta, double t_next, double dt, double src, hipStream_t st) {
+  switch (p->epl) {
+    case 1: return launch_adj_e<NP, NS, 1>(p, win, wout, usnap, eta, t_next, dt, src, st);
+    case 4:
+      if constexpr (NP <= 5)
+        return launch_adj_e<NP, NS, 4>(p, win, wout, usnap, eta, t_next, dt, src, st);
+      [[fallthrough]];
+    default: return launch_adj_e<NP, NS, 2>(p, win, wout, usnap, eta, t_next, dt, src, st);
+  }
 }
 
 // Dispatch on Np (2..9) and the number of stages.
@@ -749,8 +1050,8 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   *out = nullptr;
   if (N < 1 || N > kMaxNP - 1) return fail(DG_ERR_ARG, "N must be in 1..8");
   if (K < 2 || batch < 1) return fail(DG_ERR_ARG, "need K >= 2 and batch >= 1");
-  if (K > INT32_MAX || K * batch > (int64_t(1) << 40))
-    return fail(DG_ERR_ARG, "K*batch too large");
+  if (K * batch >= (int64_t(1) << 31) - 4096)
+    return fail(DG_ERR_ARG, "batch*K must stay below 2^31 elements per plan");
   if (!r || !V || !invV || !Dr || !LIFT || !VX) return fail(DG_ERR_ARG, "null operator pointer");
   if (inflow_variant != DG_INFLOW_SIN_AT && inflow_variant != DG_INFLOW_SIN_A2T)
     return fail(DG_ERR_ARG, "bad inflow_variant");
@@ -774,6 +1075,13 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   std::memcpy(p->Dr, Dr, sizeof(double) * NP * NP);
   std::memcpy(p->LIFT, LIFT, sizeof(double) * NP * 2);
 
+  bool sym = false;
+  DG_DISPATCH_NP(p->NP, sym = make_eo<NP>(p, 1.0, nullptr));
+  if (!sym) {
+    delete p;
+    return fail(DG_ERR_ARG, "Dr/LIFT are not centro-(anti)symmetric (nodes must be symmetric)");
+  }
+
   std::vector<double> scale(K);
   double hmin = 1e300, hmax = -1e300, hsum = 0.0;
   for (int64_t k = 0; k < K; ++k) {
@@ -791,6 +1099,12 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   p->uniform = (hmax - hmin) <= 1e-12 * hmean;
   p->s_uniform = 2.0 / hmean;
 
+  {
+    if (const char* v = std::getenv("DG_ELEMS_PER_LANE")) {
+      const int k = std::atoi(v);
+      if (k == 1 || k == 2 || k == 4) p->epl = k;
+    }
+  }
   auto cleanup = [&](const std::string& m) {
     dg_plan_destroy(p);
     return fail(DG_ERR_NOMEM, m);
@@ -830,6 +1144,19 @@ int dg_plan_query(const dg_plan* p, int64_t out[6]) {
   out[4] = p->uniform ? 1 : 0;
   out[5] = p->nstages;
   return DG_OK;
+}
+
+int dg_plan_tune(dg_plan* p, int key, int64_t value) {
+  if (!p) return fail(DG_ERR_ARG, "null plan");
+  switch (key) {
+    case DG_TUNE_ELEMS_PER_LANE:
+      if (value != 1 && value != 2 && value != 4)
+        return fail(DG_ERR_ARG, "elements per lane must be 1, 2 or 4");
+      p->epl = int(value);
+      return DG_OK;
+    default:
+      return fail(DG_ERR_ARG, "unknown tuning key");
+  }
 }
 
 int dg_advec_rhs(const dg_plan* p, const double* u, double* rhs, double t, void* stream) {

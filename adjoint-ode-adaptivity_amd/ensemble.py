@@ -1,0 +1,114 @@
+"""Ensembles of independent initial conditions, sharded one process per GPU.
+
+The reference's only data-parallel axis is the ensemble of initial conditions
+(``vmap`` over ICs, python/Main_width_ref.py:466-478), reduced by a mean over ICs and
+an argmax (:479, :491).  Here each rank owns a contiguous block of ICs, runs the
+forward + adjoint sweeps for all of them as one batched plan (no data-path
+communication), reduces its per-IC indicators to one K-vector in fixed order, and the
+ranks exchange those partial sums with ONE all-gather (RCCL over xGMI on GPUs).  Every
+rank then sums the gathered slices in rank order, so the mean indicator and the refine
+index are bit-identical on all ranks regardless of the collective's internal order
+(an all-reduce would not guarantee that).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .operators import DGAdvection1D, sum_rows
+
+
+def ic_params(indices, seed_base=0):
+  """Synthetic IC family of SURVEY §8d: u0_j(x) = A_j sin(2 pi m_j x + phi_j) with
+  rng = default_rng(seed_base + j), A ~ U[0.5, 1.5], m ~ U{1..8}, phi ~ U[0, 2 pi)."""
+  amp, freq, phase = [], [], []
+  for j in indices:
+    rng = np.random.default_rng(seed_base + int(j))
+    amp.append(rng.uniform(0.5, 1.5))
+    freq.append(float(rng.integers(1, 9)))
+    phase.append(rng.uniform(0.0, 2 * np.pi))
+  return np.array(amp), np.array(freq), np.array(phase)
+
+
+def shard(n_total, rank, world):
+  """Contiguous block of IC indices owned by ``rank`` (sizes differ by at most one)."""
+  base, extra = divmod(n_total, world)
+  start = rank * base + min(rank, extra)
+  return range(start, start + base + (1 if rank < extra else 0))
+
+
+class EnsembleSweep:
+  """One forward + adjoint sweep over this rank's ICs, producing the rank's partial
+  indicator sum (K values).  J = 1/2 |u(T)|^2 per IC (terminal adjoint w^N = u^N).
+
+  All work is enqueued on torch's current stream; ``run`` does not synchronise.
+  """
+
+  def __init__(self, mesh, ic_indices, nsteps, dt, a=2 * np.pi, inflow="a", seed_base=0,
+               params=None):
+    self.ic_indices = list(ic_indices)
+    self.batch = len(self.ic_indices)
+    if self.batch < 1:
+      raise ValueError("a rank needs at least one IC")
+    self.nsteps, self.dt = int(nsteps), float(dt)
+    self.op = DGAdvection1D(mesh, a=a, batch=self.batch, inflow=inflow)
+    amp, freq, phase = params if params is not None else ic_params(self.ic_indices, seed_base)
+    self.snaps = self.op.new_field(self.nsteps + 1)
+    # u^0 lives in snapshot 0; the forward sweep with u aliasing it leaves it untouched.
+    self.op.init_sine(amp, freq, phase, out=self.snaps[0])
+    self.w = self.op.new_field()
+    self.eta = torch.zeros(self.op.ktot, dtype=torch.float64, device=self.op.device)
+    self.partial = torch.zeros(self.op.K, dtype=torch.float64, device=self.op.device)
+
+  @property
+  def dof_updates(self):
+    """DOF-updates of one sweep: nsteps forward + nsteps adjoint steps of every DOF."""
+    return 2 * self.op.Np * self.op.ktot * self.nsteps
+
+  def forward(self):
+    self.op.forward(self.snaps[0], 0.0, self.dt, self.nsteps, self.snaps)
+
+  def adjoint(self):
+    self.w.copy_(self.snaps[self.nsteps])
+    self.eta.zero_()
+    self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta)
+
+  def reduce(self):
+    sum_rows(self.eta, self.batch, out=self.partial)
+    return self.partial
+
+  def run(self):
+    self.forward()
+    self.adjoint()
+    return self.reduce()
+
+
+class DeviceReducer:
+  """Fixed-order sum and numpy-semantics argmax through the HIP library."""
+
+  def __init__(self, op):
+    self.op = op
+
+  def sum_rows(self, stacked):
+    return sum_rows(stacked.contiguous(), stacked.shape[0])
+
+  def argmax(self, x):
+    return self.op.argmax_async(x.contiguous(), use_abs=True)
+
+
+def gather_indicator(partial, n_total, reducer, group=None):
+  """All-gather the per-rank partial sums, sum them in rank order, take the mean over
+  all ICs and the argmax of its magnitude (python/Main_width_ref.py:479,491).
+  Returns (mean indicator, index tensor).  Works for any world size (1 = no collective)."""
+  if dist.is_available() and dist.is_initialized():
+    world = dist.get_world_size(group)
+  else:
+    world = 1
+  if world > 1:
+    bufs = [torch.empty_like(partial) for _ in range(world)]
+    dist.all_gather(bufs, partial.contiguous(), group=group)
+    stacked = torch.stack(bufs)
+  else:
+    stacked = partial.reshape(1, -1)
+  total = reducer.sum_rows(stacked)
+  mean = total / float(n_total)
+  return mean, reducer.argmax(mean)

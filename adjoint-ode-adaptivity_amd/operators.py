@@ -97,6 +97,14 @@ class DGAdvection1D:
   def __exit__(self, *exc):
     self.close()
 
+  def tune(self, elems_per_lane=None):
+    """Shape of the fused step kernels (results are bit-identical for every setting):
+    each lane holds ``elems_per_lane`` elements (1, 2 or 4; tile = 256 * that)."""
+    if elems_per_lane is not None:
+      _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_ELEMS_PER_LANE,
+                                        int(elems_per_lane)), "dg_plan_tune")
+    return self
+
   # --- checks ---
   def _field(self, t, name, numel=None, dtype=torch.float64):
     if not isinstance(t, torch.Tensor) or not t.is_cuda:

@@ -1,0 +1,195 @@
+"""Benchmark: DOF-updates/s of the 1D DG advection forward + adjoint sweep (BASELINE.json).
+
+One bench step = one forward sweep of --nsteps fused LSERK4 steps (snapshots stored),
+one adjoint sweep of --nsteps reverse steps accumulating the dual-weighted residual,
+the per-rank indicator reduction, the cross-rank all-gather + fixed-order sum + argmax
+(the refine decision), and the refine index copied to the host.
+
+Workload per rank = BASELINE config 2 (N=4, K=1,048,576, fp64, uniform mesh on [0,1],
+a = 2*pi, dt from One_code.mlx:111-112).  Rank 0 runs u0 = sin(2 pi x) (the golden IC);
+rank j > 0 runs IC j of the synthetic ensemble.  N GPUs = an ensemble of N
+trajectories, one per GPU (weak scaling; the only exchange is the indicator all-gather).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--nsteps S] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+  sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def parse():
+  p = argparse.ArgumentParser()
+  p.add_argument("--gpus", type=int, default=1)
+  p.add_argument("--steps", type=int, default=10)
+  p.add_argument("--warmup", type=int, default=3)
+  p.add_argument("--N", type=int, default=4)
+  p.add_argument("--K", type=int, default=1 << 20)
+  p.add_argument("--nsteps", type=int, default=20, help="time steps per sweep (each direction)")
+  p.add_argument("--no-cpu-baseline", action="store_true")
+  p.add_argument("--cpu-steps", type=int, default=6, help="time steps of the CPU sample")
+  return p.parse_args()
+
+
+def cpu_baseline(N, K, nsteps):
+  """The oracle (numpy restatement of utils/*.m + One_code.mlx, vectorised like MATLAB,
+  one thread) on a bounded sample of the same workload: `nsteps` forward + adjoint
+  steps at the full N, K."""
+  from threadpoolctl import threadpool_limits
+
+  from oracle import adjoint as oadj
+  from oracle import advec as oadv
+  from oracle import setup1d
+  S = setup1d.uniform_setup(N, K, metric="element")
+  a = 2 * np.pi
+  dt = oadv.bench_dt(S)
+  u0 = np.sin(2 * np.pi * S["x"])
+  with threadpool_limits(1):
+    t0 = time.perf_counter()
+    snaps, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, a, S)
+    oadj.adjoint_sweep(snaps[-1], snaps, times, dt, a, S)
+    el = time.perf_counter() - t0
+  dofs = 2 * (N + 1) * K * nsteps
+  return {"value": dofs / el, "unit": "DOF-updates/s", "cores": 1, "kind": "port",
+          "sample": f"{nsteps} fwd + {nsteps} adj LSERK4 steps (with DWR indicator) at N={N}, "
+                    f"K={K}, numpy oracle, 1 thread, {el:.1f} s"}
+
+
+def main():
+  args = parse()
+  import torch
+  import torch.distributed as dist
+
+  import importlib
+  pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
+  ens = pkg.ensemble
+
+  world = int(os.environ.get("WORLD_SIZE", "1"))
+  rank = int(os.environ.get("RANK", "0"))
+  local = int(os.environ.get("LOCAL_RANK", "0"))
+  torch.cuda.set_device(local)
+  if world > 1:
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+  dev = torch.device("cuda", local)
+
+  N, K, nsteps = args.N, args.K, args.nsteps
+  mesh = pkg.BaseGalerkin1D(n=N, k=K, domain=[0.0, 1.0])
+  dt = mesh.cfl_dt()
+  if rank == 0:
+    params = (np.array([1.0]), np.array([1.0]), np.array([0.0]))  # sin(2 pi x)
+  else:
+    params = ens.ic_params([rank])
+  sweep = ens.EnsembleSweep(mesh, [rank], nsteps, dt, params=params)
+  reducer = ens.DeviceReducer(sweep.op)
+  stream = torch.cuda.current_stream(dev)
+
+  def one_step(ev=None):
+    if ev:
+      ev[0].record(stream)
+    sweep.forward()
+    if ev:
+      ev[1].record(stream)
+    sweep.w.copy_(sweep.snaps[nsteps])
+    sweep.eta.zero_()
+    if ev:
+      ev[2].record(stream)
+    sweep.op.adjoint(sweep.w, sweep.snaps, 0.0, dt, nsteps, eta=sweep.eta)
+    if ev:
+      ev[3].record(stream)
+    partial = sweep.reduce()
+    _, idx = ens.gather_indicator(partial, world, reducer)
+    return int(idx.item())  # the refine index goes to the host (mesh split)
+
+  for _ in range(args.warmup):
+    one_step()
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+
+  evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+  t0 = time.perf_counter()
+  for s in range(args.steps):
+    ref_idx = one_step(evs[s])
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  elapsed = time.perf_counter() - t0
+  if world > 1:
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+  fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+  adj_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+  Np, ktot = N + 1, K
+  fwd_launch_us = fwd_ms * 1e3 / nsteps
+  adj_launch_us = adj_ms * 1e3 / nsteps
+  # Algorithmic bytes per launch: forward 16 B/DOF (read u^n, write
+  # u^{n+1}); adjoint 24 B/DOF (read w^{n+1}, read u^{n+1}, write w^n) + 16 B/element (eta rmw).
+  fwd_bytes = 16.0 * Np * ktot
+  adj_bytes = 24.0 * Np * ktot + 16.0 * ktot
+  adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
+  fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
+  traffic = None
+  traffic_src = None
+  if os.path.exists(PROFILE_TRAFFIC):
+    try:
+      with open(PROFILE_TRAFFIC) as f:
+        tr = json.load(f)
+      if tr.get("N") == N and tr.get("K") == K:
+        traffic = tr.get("adj_bytes_per_launch")
+        traffic_src = tr.get("source")
+    except (OSError, ValueError):
+      pass
+
+  total_dofs = sweep.dof_updates * world * args.steps
+  value = total_dofs / elapsed
+  out = {
+      "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
+      "value": value,
+      "unit": "DOF-updates/s",
+      "n_gpus": world,
+      "steps": args.steps,
+      "warmup": args.warmup,
+      "ms_per_step": elapsed / args.steps * 1e3,
+      "higher_is_better": True,
+      "scaling": "weak",
+      "vs_baseline": None,
+      "dtype": "f64",
+      "data": "synthetic (u0 = sin(2 pi x) on rank 0, SURVEY 8d sine-family ICs on other ranks)",
+      "config": {"workload": f"config 2: 1D DG advection N={N} K={K} LSERK4 fwd+adj "
+                             f"{nsteps}+{nsteps} steps/sweep + DWR indicator + refine argmax",
+                 "N": N, "K": K, "nsteps_per_sweep": nsteps, "trajectories_per_gpu": 1,
+                 "parallelism": f"ensemble-dp{world}"},
+      "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                   "kernel": "k_adj<5,5,true> (adjoint step + DWR)",
+                   "launch_us": adj_launch_us, "algorithmic_bytes": adj_bytes,
+                   "traffic_source": traffic_src},
+      "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": fwd_gbs / HBM_PEAK_GBS, "kernel": "k_step<5,5,true>",
+                       "launch_us": fwd_launch_us, "algorithmic_bytes": fwd_bytes},
+      "refine_index": ref_idx,
+  }
+  if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_steps)
+  if rank == 0:
+    print(json.dumps(out), flush=True)
+  if world > 1:
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+  main()

@@ -76,6 +76,12 @@ int dg_plan_destroy(dg_plan* plan);
  * out[5]=time stages per step. */
 int dg_plan_query(const dg_plan* plan, int64_t out[6]);
 
+/* Tuning knob of the fused step kernels (results are bit-identical for every setting).
+ *   DG_TUNE_ELEMS_PER_LANE  elements held per lane: 1, 2 or 4 (tile = 256*value elements)
+ * Environment override at plan creation: DG_ELEMS_PER_LANE. */
+enum { DG_TUNE_ELEMS_PER_LANE = 1 };
+int dg_plan_tune(dg_plan* plan, int key, int64_t value);
+
 /* rhs = AdvecRHS1D(u, t, a)   — utils/AdvecRHS1D.m:1-20 (inline copy One_code.mlx:124-134).
  * Central flux (alpha = 1), inflow at each trajectory's x = 0, du = 0 at the outflow face. */
 int dg_advec_rhs(const dg_plan* plan, const double* u, double* rhs, double t, void* stream);
@@ -83,7 +89,8 @@ int dg_advec_rhs(const dg_plan* plan, const double* u, double* rhs, double t, vo
 /* Forward sweep: nsteps fused steps of the plan's integrator starting at time t0
  * (the "dg_march" role; LSERK4 loop One_code.mlx:106-140, time = time + dt as there).
  * u (in/out): the state.  snapshots (nullable): (nsteps+1) consecutive states,
- * snapshots[n] = u^n; u may alias snapshots (then u^0 is not copied). */
+ * snapshots[n] = u^n.  u may alias snapshots[0]: then u^0 is neither copied nor
+ * overwritten (u keeps u^0) and the final state is snapshots[nsteps]. */
 int dg_lserk4_fwd(dg_plan* plan, double* u, double t0, double dt, int nsteps,
                   double* snapshots, void* stream);
 

@@ -1,0 +1,65 @@
+"""In-process A/B of the step-kernel shapes (cdna_hip_programming.md §5.4 rule 24):
+interleaved rounds, median per-launch time of the forward and adjoint kernels.
+
+  python profiles/ab_variants.py [--N 4] [--K 1048576] [--nsteps 20] [--rounds 5]
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+  p = argparse.ArgumentParser()
+  p.add_argument("--N", type=int, default=4)
+  p.add_argument("--K", type=int, default=1 << 20)
+  p.add_argument("--nsteps", type=int, default=20)
+  p.add_argument("--rounds", type=int, default=5)
+  p.add_argument("--variants", default="1,2,4")
+  a = p.parse_args()
+  pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
+  mesh = pkg.BaseGalerkin1D(n=a.N, k=a.K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  dt = mesh.cfl_dt()
+  snaps = op.new_field(a.nsteps + 1)
+  op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
+  w = op.new_field()
+  eta = torch.zeros(op.ktot, dtype=torch.float64, device=op.device)
+  variants = [int(v) for v in a.variants.split(",")]
+  res = {v: {"fwd": [], "adj": []} for v in variants}
+  st = torch.cuda.current_stream()
+  for r in range(a.rounds + 1):
+    for v in variants:
+      op.tune(elems_per_lane=v)
+      e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+      e[0].record(st)
+      op.forward(snaps[0], 0.0, dt, a.nsteps, snaps)
+      e[1].record(st)
+      w.copy_(snaps[a.nsteps])
+      op.adjoint(w, snaps, 0.0, dt, a.nsteps, eta=eta)
+      e[2].record(st)
+      torch.cuda.synchronize()
+      if r > 0:  # round 0 is warm-up
+        res[v]["fwd"].append(e[0].elapsed_time(e[1]) * 1e3 / a.nsteps)
+        res[v]["adj"].append(e[1].elapsed_time(e[2]) * 1e3 / a.nsteps)
+  Np = a.N + 1
+  fb, ab = 16.0 * Np * a.K, 24.0 * Np * a.K + 16.0 * a.K
+  out = {}
+  for v in variants:
+    f, d = float(np.median(res[v]["fwd"])), float(np.median(res[v]["adj"]))
+    out[f"elems_per_lane={v}"] = {"fwd_us": f, "fwd_GBs": fb / f / 1e3, "adj_us": d,
+                                         "adj_GBs": ab / d / 1e3,
+                                         "fwd_min_us": float(np.min(res[v]["fwd"])),
+                                         "adj_min_us": float(np.min(res[v]["adj"]))}
+  print(json.dumps({"N": a.N, "K": a.K, "nsteps": a.nsteps, "results": out}, indent=1))
+
+
+if __name__ == "__main__":
+  main()

@@ -1,0 +1,74 @@
+"""Summarise rocprofv3 CSV output (kernel stats + FETCH_SIZE / WRITE_SIZE passes) into
+one JSON per round, and derive the per-launch HBM traffic of the hot kernels.
+
+  python profiles/summarize.py --stats <kernel_stats.csv> --fetch <counter_collection.csv>
+         --write <counter_collection.csv> --out profiles/rNN/summary.json [--traffic-json profiles/pmc_traffic.json]
+
+Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reads exactly half of the bytes of a 16-B/lane coalesced stream, so the read
+side is doubled; WRITE_SIZE is exact for 16-B/lane stores.
+"""
+import argparse
+import collections
+import csv
+import json
+import re
+
+
+def short(name):
+  name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+  m = re.match(r"([A-Za-z_:0-9]+)(<[^(]*>)?", name)
+  return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+
+
+def counters(path, counter):
+  agg = collections.defaultdict(list)
+  for r in csv.DictReader(open(path)):
+    if r["Counter_Name"] == counter:
+      agg[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+  return agg
+
+
+def main():
+  p = argparse.ArgumentParser()
+  p.add_argument("--stats", required=True)
+  p.add_argument("--fetch")
+  p.add_argument("--write")
+  p.add_argument("--out", required=True)
+  p.add_argument("--traffic-json")
+  p.add_argument("--N", type=int, default=4)
+  p.add_argument("--K", type=int, default=1 << 20)
+  a = p.parse_args()
+  out = collections.OrderedDict()
+  for r in csv.DictReader(open(a.stats)):
+    out[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
+                             "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3,
+                             "pct": float(r["Percentage"])}
+  for path, cnt, scale in ((a.fetch, "FETCH_SIZE", 2.0), (a.write, "WRITE_SIZE", 1.0)):
+    if not path:
+      continue
+    for k, v in counters(path, cnt).items():
+      d = out.setdefault(k, {})
+      d[cnt + "_KiB_avg"] = sum(v) / len(v)
+      d[cnt.split("_")[0].lower() + "_bytes_corrected"] = scale * 1024.0 * sum(v) / len(v)
+  json.dump(out, open(a.out, "w"), indent=1)
+  print(json.dumps(out, indent=1))
+  if a.traffic_json:
+    def hbm(key):
+      d = out.get(key, {})
+      if "fetch_bytes_corrected" in d and "write_bytes_corrected" in d:
+        return d["fetch_bytes_corrected"] + d["write_bytes_corrected"]
+      return None
+    adj = [k for k in out if k.startswith("k_adj")]
+    fwd = [k for k in out if k.startswith("k_step")]
+    tr = {"N": a.N, "K": a.K, "source": a.out,
+          "adj_kernel": adj[0] if adj else None,
+          "adj_bytes_per_launch": hbm(adj[0]) if adj else None,
+          "fwd_kernel": fwd[0] if fwd else None,
+          "fwd_bytes_per_launch": hbm(fwd[0]) if fwd else None,
+          "note": "FETCH_SIZE x2 (gfx950 16-B/lane half count) + WRITE_SIZE, KiB->bytes"}
+    json.dump(tr, open(a.traffic_json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+  main()

@@ -325,3 +325,24 @@ def test_full_size_config2_forward_adjoint(pkg, gpu):
   assert rel_err(setup1d.from_elem_major(host(w), N + 1), w_ref) <= RTOL
   assert rel_err(host(eta), eta_ref) <= RTOL
   assert op.argmax(eta) == int(np.argmax(np.abs(host(eta))))
+
+
+@pytest.mark.parametrize("N,K", [(4, 3000), (2, 20000), (8, 1111)])
+def test_kernel_variants_bit_identical(pkg, gpu, N, K):
+  """Every step-kernel shape (elements per lane 1, 2, 4) gives the same bits."""
+  import torch
+  S, mesh = mesh_pair(pkg, N, K)
+  u0 = dev(setup1d.to_elem_major(np.sin(2 * np.pi * S["x"]) + 0.1 * np.cos(40 * S["x"])), gpu)
+  dt = oadv.bench_dt(S)
+  outs = []
+  for epl in (1, 2, 4):
+    op = make_op(pkg, mesh).tune(elems_per_lane=epl)
+    snaps = op.new_field(5)
+    op.forward(u0.clone(), 0.0, dt, 4, snaps)
+    w = snaps[4].clone()
+    eta = torch.zeros(K, dtype=torch.float64, device=gpu)
+    op.adjoint(w, snaps, 0.0, dt, 4, src_coef=0.3, eta=eta)
+    outs.append((host(snaps), host(w), host(eta)))
+  for o in outs[1:]:
+    for a_, b_ in zip(outs[0], o):
+      np.testing.assert_array_equal(a_, b_)
