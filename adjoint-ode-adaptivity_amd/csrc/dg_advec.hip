@@ -109,20 +109,23 @@ template <int NP> struct EOArgs {
   double lo[NO];
 };
 
-template <int NP, int NS> struct StepArgs {
+// Arguments of a launch that advances MS time steps of NS stages each.
+template <int NP, int NS, int MS> struct StepArgs {
   EOArgs<NP> op;
-  double sc;          // dt * s (uniform mesh) or dt (non-uniform: times scale[k])
-  double uin[NS];     // inflow value at each stage time
-  int64_t ktot;       // batch * K elements
-  int32_t K;          // elements per trajectory
+  double sc;            // dt (non-uniform meshes multiply by scale[k]; uniform: folded in op)
+  double uin[MS * NS];  // inflow value at each stage time
+  int64_t ktot;         // batch * K elements
+  int64_t stride;       // doubles between consecutive snapshots
+  int32_t K;            // elements per trajectory
 };
 
-template <int NP> struct AdjArgs {
+template <int NP, int MS> struct AdjArgs {
   EOArgs<NP> op;
-  double sc;          // as StepArgs
-  double uin_res;     // inflow value at t_{n+1} for the residual
-  double src;         // functional source coefficient for node n+1
+  double sc;
+  double uin_res[MS];  // inflow value at t_{n+st+1} for the residual of step st
+  double src[MS];      // functional source coefficient for node n+st+1
   int64_t ktot;
+  int64_t stride;      // doubles between consecutive snapshots
   int32_t K;
   int32_t has_eta;
 };
@@ -251,28 +254,84 @@ __device__ __forceinline__ Elem elem_info(int64_t e0, int el, int64_t ktot, int3
   return E;
 }
 
+// Even/odd element state helpers.
+template <int NP>
+__device__ __forceinline__ void to_eo(const double* u, double* ev, double* od) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    ev[k] = 0.5 * (u[k] + u[N - k]);
+    od[k] = 0.5 * (u[k] - u[N - k]);
+  }
+  if constexpr (NE > NO) ev[NO] = u[NO];
+}
+
+template <int NP>
+__device__ __forceinline__ void from_eo(const double* ev, const double* od, double* u) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    u[k] = ev[k] + od[k];
+    u[N - k] = ev[k] - od[k];
+  }
+  if constexpr (NE > NO) u[NO] = ev[NO];
+}
+
+// Write the TE interior elements of the tile (element-major, nodal) through the LDS
+// image with 16-byte stores.  Callers barrier before (face reads done) and after (when
+// the image is reused).
+template <int NP, int EPL, int H>
+__device__ __forceinline__ void stage_out(double* __restrict__ lds, const double (*ev)[(NP + 1) / 2],
+                                          const double (*od)[NP / 2], bool dual) {
+  constexpr int T = kBlock * EPL;
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int m = 0; m < EPL; ++m) {
+    const int el = m * kBlock + lane;
+    if (el >= H && el < T - H) {
+      double* o = lds + (el - H) * NP;
+      if (dual) {  // dual coordinates back to nodal: w_k = (we+wo)/2, w_{N-k} = (we-wo)/2
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          o[k] = 0.5 * (ev[m][k] + od[m][k]);
+          o[N - k] = 0.5 * (ev[m][k] - od[m][k]);
+        }
+        if constexpr (NE > NO) o[NO] = ev[m][NO];
+      } else {
+        from_eo<NP>(ev[m], od[m], o);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
-// Forward fused step: all NS stages of AdvecRHS1D + the low-storage update for the EPL
-// elements of each lane.  UNI: the operator constants already carry dt*2/h.
+// Forward fused kernel: MS time steps of NS stages (AdvecRHS1D + the low-storage update)
+// for the EPL elements of each lane.  After each step st the interior elements go to
+// snap + st*stride (if snap) and after the last step also to `last` (if non-null).
+// UNI: the operator constants already carry dt*2/h.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int EPL>
+template <int NP, int NS, bool UNI, int EPL, int MS>
 __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
-                                                 double* __restrict__ uout,
-                                                 double* __restrict__ uout2,
+                                                 double* __restrict__ snap,
+                                                 double* __restrict__ last,
                                                  const double* __restrict__ scale,
-                                                 StepArgs<NP, NS> args) {
+                                                 StepArgs<NP, NS, MS> args) {
   using G = TileGeo<NP, EPL>;
   constexpr int T = G::T;
-  constexpr int H = NS;          // dependency cone grows one element per stage
+  constexpr int H = MS * NS;     // dependency cone: one element per stage
   constexpr int TE = T - 2 * H;  // output elements per tile (even)
-  static_assert(TE % 2 == 0, "tile output must be 16-byte aligned");
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int lane = threadIdx.x;
   const int64_t tile = blockIdx.x;
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
+  const int64_t o0 = tile * TE * NP;
+  const int64_t rem = nd - o0;
+  const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
 
-  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   TileRegs<NP, EPL> pf;
   tile_issue<NP, EPL>(uin, e0, nd, pf);
   tile_commit<NP, EPL>(pf, lds);
@@ -283,15 +342,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
     const int el = m * kBlock + lane;
-    double u[NP];
-#pragma unroll
-    for (int i = 0; i < NP; ++i) u[i] = lds[pf.off + el * NP + i];
-#pragma unroll
-    for (int k = 0; k < NO; ++k) {
-      ev[m][k] = 0.5 * (u[k] + u[N - k]);
-      od[m][k] = 0.5 * (u[k] - u[N - k]);
-    }
-    if constexpr (NE > NO) ev[m][NO] = u[NO];
+    to_eo<NP>(lds + pf.off + el * NP, ev[m], od[m]);
     E[m] = elem_info<H, T>(e0, el, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
@@ -300,122 +351,107 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
 
   double re[EPL][NE], ro[EPL][NO];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int fL = (s & 1) * 2 * (T + 2);  // faceL = lds[fL ...], faceR = lds[fR ...]
-    const int fR = fL + (T + 2);
-    double u0[EPL], uN[EPL];
+  for (int st = 0; st < MS; ++st) {
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) {
-      const int el = m * kBlock + lane;
-      u0[m] = ev[m][0] + od[m][0];
-      uN[m] = ev[m][0] - od[m][0];
-      lds[fL + el + 1] = u0[m];
-      lds[fR + el + 1] = uN[m];
+    for (int s = 0; s < NS; ++s) {
+      const int fL = (s & 1) * 2 * (T + 2);  // faceL = lds[fL ...], faceR = lds[fR ...]
+      const int fR = fL + (T + 2);
+      double u0[EPL], uN[EPL];
+#pragma unroll
+      for (int m = 0; m < EPL; ++m) {
+        const int el = m * kBlock + lane;
+        u0[m] = ev[m][0] + od[m][0];
+        uN[m] = ev[m][0] - od[m][0];
+        lds[fL + el + 1] = u0[m];
+        lds[fR + el + 1] = uN[m];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < EPL; ++m) {
+        const int el = m * kBlock + lane;
+        // faceR[el] is element el-1's right node, faceL[el+2] element el+1's left node; the
+        // pad entries are only read by the outermost halo elements, whose results are dropped.
+        const double uL = E[m].first ? args.uin[st * NS + s] : lds[fR + el];
+        const double uR = lds[fL + el + 2];
+        const double du0 = u0[m] - uL;
+        const double du1 = E[m].last ? 0.0 : (uN[m] - uR);
+        const double dlt = du0 - du1, sig = du0 + du1;
+        double ae[NE], ao[NO];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          double t = args.op.le[k] * dlt;
+#pragma unroll
+          for (int j = 0; j < NO; ++j) t = fma(args.op.Qeo[k * NO + j], od[m][j], t);
+          ae[k] = UNI ? t : sc[m] * t;
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          double t = args.op.lo[k] * sig;
+#pragma unroll
+          for (int j = 0; j < NE; ++j) t = fma(args.op.Qoe[k * NE + j], ev[m][j], t);
+          ao[k] = UNI ? t : sc[m] * t;
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          re[m][k] = (s == 0) ? ae[k] : fma(RK<NS>::A(s), re[m][k], ae[k]);  // rk4a(1) = 0
+          ev[m][k] = fma(RK<NS>::B(s), re[m][k], ev[m][k]);
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          ro[m][k] = (s == 0) ? ao[k] : fma(RK<NS>::A(s), ro[m][k], ao[k]);
+          od[m][k] = fma(RK<NS>::B(s), ro[m][k], od[m][k]);
+        }
+      }
     }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < EPL; ++m) {
-      const int el = m * kBlock + lane;
-      // faceR[el] is element el-1's right node, faceL[el+2] element el+1's left node; the
-      // pad entries are only read by the outermost halo elements, whose results are dropped.
-      const double uL = E[m].first ? args.uin[s] : lds[fR + el];
-      const double uR = lds[fL + el + 2];
-      const double du0 = u0[m] - uL;
-      const double du1 = E[m].last ? 0.0 : (uN[m] - uR);
-      const double dlt = du0 - du1, sig = du0 + du1;
-      double ae[NE], ao[NO];
-#pragma unroll
-      for (int k = 0; k < NE; ++k) {
-        double t = args.op.le[k] * dlt;
-#pragma unroll
-        for (int j = 0; j < NO; ++j) t = fma(args.op.Qeo[k * NO + j], od[m][j], t);
-        ae[k] = UNI ? t : sc[m] * t;
-      }
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        double t = args.op.lo[k] * sig;
-#pragma unroll
-        for (int j = 0; j < NE; ++j) t = fma(args.op.Qoe[k * NE + j], ev[m][j], t);
-        ao[k] = UNI ? t : sc[m] * t;
-      }
-#pragma unroll
-      for (int k = 0; k < NE; ++k) {
-        re[m][k] = (s == 0) ? ae[k] : fma(RK<NS>::A(s), re[m][k], ae[k]);  // rk4a(1) = 0
-        ev[m][k] = fma(RK<NS>::B(s), re[m][k], ev[m][k]);
-      }
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        ro[m][k] = (s == 0) ? ao[k] : fma(RK<NS>::A(s), ro[m][k], ao[k]);
-        od[m][k] = fma(RK<NS>::B(s), ro[m][k], od[m][k]);
-      }
-    }
-  }
-
-  __syncthreads();  // the last stage's face reads are done before the image is rewritten
-#pragma unroll
-  for (int m = 0; m < EPL; ++m) {
-    const int el = m * kBlock + lane;
-    if (el >= H && el < T - H) {
-      double* o = lds + (el - H) * NP;
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        o[k] = ev[m][k] + od[m][k];
-        o[N - k] = ev[m][k] - od[m][k];
-      }
-      if constexpr (NE > NO) o[NO] = ev[m][NO];
+    if (snap != nullptr || st == MS - 1) {
+      __syncthreads();  // the last stage's face reads are done before the image is rewritten
+      stage_out<NP, EPL, H>(lds, ev, od, false);
+      __syncthreads();
+      if (snap != nullptr) store_run(snap + st * args.stride, o0, count, lds);
+      if (st == MS - 1 && last != nullptr) store_run(last, o0, count, lds);
+      if (st < MS - 1) __syncthreads();  // the next stage's faces alias the image
     }
   }
-  __syncthreads();
-  const int64_t o0 = tile * TE * NP;
-  const int64_t rem = nd - o0;
-  const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
-  store_run(uout, o0, count, lds);
-  if (uout2 != nullptr) store_run(uout2, o0, count, lds);
 }
 
 // ---------------------------------------------------------------------------
-// Adjoint fused step: w^n = S^T (w^{n+1} + src*u^{n+1}) and the DWR contribution.
-// Reverse of stage s (forward: r = A_s r + dt L u ; u = u + B_s r):
-//   lr += B_s lu ;  lu += dt L^T lr ;  lr = A_s lr
-// L^T per element with q = sc*lr, g0 = L0.q, g1 = L1.q:
-//   (L^T)_j = sum_i Dm[i][j] q_i + [j=0](g0 - g1_{left}) + [j=N]([!last] g1 - [!last] g0_{right})
-// Indicator: eta += dt * sum_i w_i * s*(L0_i du0 + L1_i du1) = sc*(du0*(L0.w) + du1*(L1.w)).
+// Adjoint fused kernel: MS reverse steps st = MS-1..0, each
+//   w^{n+st+1} += src_st * u^{n+st+1};  eta += DWR(u^{n+st+1}, w^{n+st+1});  w^{n+st} = S^T w^{n+st+1}
+// with u^{n+st+1} = snap + st*stride.  Reverse of stage s (forward: r = A_s r + dt L u ;
+// u = u + B_s r):  lr += B_s lu ;  lu += dt L^T lr ;  lr = A_s lr.
+// The adjoint lives in the dual even/odd coordinates (the transpose of the inverse
+// transform): we_k = w_k + w_{N-k}, wo_k = w_k - w_{N-k}, we_NO = w_mid.
+// Indicator: eta += dt * sum_i w_i * s*(L0_i du0 + L1_i du1), with L0.w = le.we + lo.wo and
+// L1.w = -le.we + lo.wo.  The next snapshot tile is prefetched during each step's stages.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int EPL>
+template <int NP, int NS, bool UNI, int EPL, int MS>
 __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
                                                 double* __restrict__ wout,
-                                                const double* __restrict__ usnap,
+                                                const double* __restrict__ snap,
                                                 double* __restrict__ eta,
                                                 const double* __restrict__ scale,
-                                                AdjArgs<NP> args) {
+                                                AdjArgs<NP, MS> args) {
   using G = TileGeo<NP, EPL>;
   constexpr int T = G::T;
-  constexpr int H = NS;
+  constexpr int H = MS * NS;
   constexpr int TE = T - 2 * H;
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int lane = threadIdx.x;
   const int64_t tile = blockIdx.x;
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
-  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   TileRegs<NP, EPL> pw, pu;
   tile_issue<NP, EPL>(win, e0, nd, pw);
-  tile_issue<NP, EPL>(usnap, e0, nd, pu);
-  // The adjoint lives in the dual even/odd coordinates (the transpose of the inverse
-  // transform): we_k = w_k + w_{N-k}, wo_k = w_k - w_{N-k}, we_NO = w_mid; back with
-  // w_k = (we_k + wo_k)/2, w_{N-k} = (we_k - wo_k)/2.  The adjoint tile is staged and read
-  // out first, then the snapshot tile, through one LDS image; the face arrays of the
-  // stages alias it afterwards.
+  tile_issue<NP, EPL>(snap + (MS - 1) * args.stride, e0, nd, pu);
   tile_commit<NP, EPL>(pw, lds);
   __syncthreads();
   double we[EPL][NE], wo[EPL][NO];
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
-    const int el = m * kBlock + lane;
-    double w[NP];
-#pragma unroll
-    for (int i = 0; i < NP; ++i) w[i] = lds[pw.off + el * NP + i];
+    const double* w = lds + pw.off + (m * kBlock + lane) * NP;
 #pragma unroll
     for (int k = 0; k < NO; ++k) {
       we[m][k] = w[k] + w[N - k];
@@ -423,134 +459,129 @@ __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
     }
     if constexpr (NE > NO) we[m][NO] = w[NO];
   }
-  __syncthreads();
-  tile_commit<NP, EPL>(pu, lds);
-  __syncthreads();
 
   Elem E[EPL];
   double sc[EPL];
-  double contrib[EPL];
+  double eacc[EPL];
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
-    const int el = m * kBlock + lane;
-    E[m] = elem_info<H, T>(e0, el, args.ktot, args.K);
+    E[m] = elem_info<H, T>(e0, m * kBlock + lane, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
+    eacc[m] = 0.0;
+  }
+
+#pragma unroll
+  for (int st = MS - 1; st >= 0; --st) {
+    __syncthreads();  // previous reads of the image (w tile or the last stage's faces) done
+    tile_commit<NP, EPL>(pu, lds);
     const int off = pu.off;
-    const double* us = lds + off + el * NP;
-    if (args.src != 0.0) {  // functional source K^{n+1} = src * u^{n+1} (dual coordinates)
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        we[m][k] = fma(args.src, us[k] + us[N - k], we[m][k]);
-        wo[m][k] = fma(args.src, us[k] - us[N - k], wo[m][k]);
-      }
-      if constexpr (NE > NO) we[m][NO] = fma(args.src, us[NO], we[m][NO]);
-    }
-    contrib[m] = 0.0;
-    if (args.has_eta) {
-      // Neighbour face values of the snapshot for the jump residual.
-      const double usL = (el > 0) ? lds[off + (el - 1) * NP + (NP - 1)] : us[0];
-      const double usR = (el < T - 1) ? lds[off + (el + 1) * NP] : us[NP - 1];
-      const double du0 = us[0] - (E[m].first ? args.uin_res : usL);
-      const double du1 = E[m].last ? 0.0 : (us[NP - 1] - usR);
-      // L0.w = le.we + lo.wo and L1.w = -le.we + lo.wo
-      double pe = 0.0, po = 0.0;
-#pragma unroll
-      for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[m][k], pe);
-#pragma unroll
-      for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[m][k], po);
-      contrib[m] = fma(du0 - du1, pe, (du0 + du1) * po);
-      if constexpr (!UNI) contrib[m] *= sc[m];
-    }
-  }
-  __syncthreads();  // the face arrays below alias the staging image
-
-  double le_[EPL][NE], lo_[EPL][NO];  // the stage residual's adjoint
-#pragma unroll
-  for (int m = 0; m < EPL; ++m) {
-#pragma unroll
-    for (int k = 0; k < NE; ++k) le_[m][k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < NO; ++k) lo_[m][k] = 0.0;
-  }
-
-#pragma unroll
-  for (int ss = 0; ss < NS; ++ss) {
-    const int s = NS - 1 - ss;
-    const int f0 = (ss & 1) * 2 * (T + 2);  // g0 = lds[f0 ...], g1 = lds[f1 ...]
-    const int f1 = f0 + (T + 2);
-    double qe[EPL][NE], qo[EPL][NO];
-    double g0[EPL], g1[EPL];
-#pragma unroll
-    for (int m = 0; m < EPL; ++m) {
-      const int el = m * kBlock + lane;
-      double gd = 0.0, gs = 0.0;
-#pragma unroll
-      for (int k = 0; k < NE; ++k) {
-        le_[m][k] = fma(RK<NS>::B(s), we[m][k], le_[m][k]);
-        qe[m][k] = UNI ? le_[m][k] : sc[m] * le_[m][k];
-        gd = fma(args.op.le[k], qe[m][k], gd);
-      }
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        lo_[m][k] = fma(RK<NS>::B(s), wo[m][k], lo_[m][k]);
-        qo[m][k] = UNI ? lo_[m][k] : sc[m] * lo_[m][k];
-        gs = fma(args.op.lo[k], qo[m][k], gs);
-      }
-      // adjoints of du0 and du1 (du0 - du1 feeds the even part, du0 + du1 the odd part)
-      g0[m] = gd + gs;
-      g1[m] = E[m].last ? 0.0 : (gs - gd);
-      lds[f0 + el + 1] = g0[m];
-      lds[f1 + el + 1] = g1[m];
-    }
     __syncthreads();
+    if (st > 0) tile_issue<NP, EPL>(snap + (st - 1) * args.stride, e0, nd, pu);
 #pragma unroll
     for (int m = 0; m < EPL; ++m) {
       const int el = m * kBlock + lane;
-      // du0 = u_0 - (left neighbour's u_N); du1 = u_N - (right neighbour's u_0), with
-      // u_0 = e_0 + o_0 and u_N = e_0 - o_0.
-      const double gl = E[m].first ? 0.0 : lds[f1 + el];      // g1 of element k-1
-      const double gr = E[m].last ? 0.0 : lds[f0 + el + 2];   // g0 of element k+1
+      const double* us = lds + off + el * NP;
+      if (args.src[st] != 0.0) {  // functional source (dual coordinates)
 #pragma unroll
-      for (int j = 0; j < NE; ++j) {
-        double t = we[m][j];
-#pragma unroll
-        for (int k = 0; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[m][k], t);
-        we[m][j] = t;
+        for (int k = 0; k < NO; ++k) {
+          we[m][k] = fma(args.src[st], us[k] + us[N - k], we[m][k]);
+          wo[m][k] = fma(args.src[st], us[k] - us[N - k], wo[m][k]);
+        }
+        if constexpr (NE > NO) we[m][NO] = fma(args.src[st], us[NO], we[m][NO]);
       }
+      if (args.has_eta) {
+        // Neighbour face values of the snapshot for the jump residual.
+        const double usL = (el > 0) ? lds[off + (el - 1) * NP + (NP - 1)] : us[0];
+        const double usR = (el < T - 1) ? lds[off + (el + 1) * NP] : us[NP - 1];
+        const double du0 = us[0] - (E[m].first ? args.uin_res[st] : usL);
+        const double du1 = E[m].last ? 0.0 : (us[NP - 1] - usR);
+        double pe = 0.0, po = 0.0;
 #pragma unroll
-      for (int j = 0; j < NO; ++j) {
-        double t = wo[m][j];
+        for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[m][k], pe);
 #pragma unroll
-        for (int k = 0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[m][k], t);
-        wo[m][j] = t;
+        for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[m][k], po);
+        double c = fma(du0 - du1, pe, (du0 + du1) * po);
+        if constexpr (!UNI) c *= sc[m];
+        eacc[m] += c;
       }
-      we[m][0] += (g0[m] + g1[m]) - (gr + gl);
-      wo[m][0] += (g0[m] - g1[m]) + (gr - gl);
+    }
+    __syncthreads();  // the face arrays below alias the staging image
+
+    double le_[EPL][NE], lo_[EPL][NO];  // the stage residual's adjoint
 #pragma unroll
-      for (int k = 0; k < NE; ++k) le_[m][k] = RK<NS>::A(s) * le_[m][k];
+    for (int m = 0; m < EPL; ++m) {
 #pragma unroll
-      for (int k = 0; k < NO; ++k) lo_[m][k] = RK<NS>::A(s) * lo_[m][k];
+      for (int k = 0; k < NE; ++k) le_[m][k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < NO; ++k) lo_[m][k] = 0.0;
+    }
+#pragma unroll
+    for (int ss = 0; ss < NS; ++ss) {
+      const int s = NS - 1 - ss;
+      const int f0 = (ss & 1) * 2 * (T + 2);  // g0 = lds[f0 ...], g1 = lds[f1 ...]
+      const int f1 = f0 + (T + 2);
+      double qe[EPL][NE], qo[EPL][NO];
+      double g0[EPL], g1[EPL];
+#pragma unroll
+      for (int m = 0; m < EPL; ++m) {
+        const int el = m * kBlock + lane;
+        double gd = 0.0, gs = 0.0;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          le_[m][k] = fma(RK<NS>::B(s), we[m][k], le_[m][k]);
+          qe[m][k] = UNI ? le_[m][k] : sc[m] * le_[m][k];
+          gd = fma(args.op.le[k], qe[m][k], gd);
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          lo_[m][k] = fma(RK<NS>::B(s), wo[m][k], lo_[m][k]);
+          qo[m][k] = UNI ? lo_[m][k] : sc[m] * lo_[m][k];
+          gs = fma(args.op.lo[k], qo[m][k], gs);
+        }
+        // adjoints of du0 and du1 (du0 - du1 feeds the even part, du0 + du1 the odd part)
+        g0[m] = gd + gs;
+        g1[m] = E[m].last ? 0.0 : (gs - gd);
+        lds[f0 + el + 1] = g0[m];
+        lds[f1 + el + 1] = g1[m];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < EPL; ++m) {
+        const int el = m * kBlock + lane;
+        // du0 = u_0 - (left neighbour's u_N); du1 = u_N - (right neighbour's u_0), with
+        // u_0 = e_0 + o_0 and u_N = e_0 - o_0.
+        const double gl = E[m].first ? 0.0 : lds[f1 + el];     // g1 of element k-1
+        const double gr = E[m].last ? 0.0 : lds[f0 + el + 2];  // g0 of element k+1
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+          double t = we[m][j];
+#pragma unroll
+          for (int k = 0; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[m][k], t);
+          we[m][j] = t;
+        }
+#pragma unroll
+        for (int j = 0; j < NO; ++j) {
+          double t = wo[m][j];
+#pragma unroll
+          for (int k = 0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[m][k], t);
+          wo[m][j] = t;
+        }
+        we[m][0] += (g0[m] + g1[m]) - (gr + gl);
+        wo[m][0] += (g0[m] - g1[m]) + (gr - gl);
+#pragma unroll
+        for (int k = 0; k < NE; ++k) le_[m][k] = RK<NS>::A(s) * le_[m][k];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) lo_[m][k] = RK<NS>::A(s) * lo_[m][k];
+      }
     }
   }
 
 #pragma unroll
   for (int m = 0; m < EPL; ++m)
-    if (args.has_eta && E[m].valid) eta[E[m].e] += contrib[m];
+    if (args.has_eta && E[m].valid) eta[E[m].e] += eacc[m];
   __syncthreads();  // the last stage's face reads are done before the image is rewritten
-#pragma unroll
-  for (int m = 0; m < EPL; ++m) {
-    const int el = m * kBlock + lane;
-    if (el >= H && el < T - H) {
-      double* o = lds + (el - H) * NP;
-#pragma unroll
-      for (int k = 0; k < NO; ++k) {
-        o[k] = 0.5 * (we[m][k] + wo[m][k]);
-        o[N - k] = 0.5 * (we[m][k] - wo[m][k]);
-      }
-      if constexpr (NE > NO) o[NO] = we[m][NO];
-    }
-  }
+  stage_out<NP, EPL, H>(lds, we, wo, true);
   __syncthreads();
   const int64_t o0 = tile * TE * NP;
   const int64_t rem = nd - o0;
@@ -823,11 +854,13 @@ struct dg_plan {
       LIFT[kMaxNP * 2];
   double* d_scale = nullptr;  // K: 2/h_k
   double* d_VX = nullptr;     // K+1
-  double* d_scratch = nullptr;
+  double* d_scratch = nullptr;   // two fields: adjoint ping-pong lands the last launch in w
+  double* d_scratch2 = nullptr;
   double* d_pv = nullptr;
   int64_t* d_pi = nullptr;
   // tuning (dg_plan_tune): elements per lane of the step kernels (tile = 256*epl elements)
   int epl = 1;
+  int msteps = 4;  // time steps fused per launch (1, 2 or 4)
 };
 
 namespace {
@@ -924,75 +957,79 @@ template <int NP> LimArgs<NP> make_lim(const dg_plan* p) {
 
 inline unsigned grid_for(int64_t n, int64_t per) { return unsigned((n + per - 1) / per); }
 
-template <int NP, int NS, int EPL>
-int launch_step_e(const dg_plan* p, const double* in, double* out, double* out2, double t,
-                  double dt, hipStream_t st) {
-  StepArgs<NP, NS> a;
+template <int NP, int NS, int EPL, int MS>
+int launch_step_e(const dg_plan* p, const double* in, double* snap, double* last,
+                  const double* times, double dt, hipStream_t st) {
+  StepArgs<NP, NS, MS> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
   a.sc = dt;  // non-uniform meshes multiply by scale[k] in the kernel
-  for (int s = 0; s < NS; ++s) a.uin[s] = inflow_value(p, t + RK<NS>::C(s) * dt);
+  for (int m = 0; m < MS; ++m)
+    for (int s = 0; s < NS; ++s) a.uin[m * NS + s] = inflow_value(p, times[m] + RK<NS>::C(s) * dt);
   a.ktot = p->ktot;
+  a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
-  constexpr int TE = kBlock * EPL - 2 * NS;
+  constexpr int TE = kBlock * EPL - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_step<NP, NS, true, EPL>), dim3(grid), dim3(kBlock), 0, st, in, out,
-                       out2, p->d_scale, a);
+    hipLaunchKernelGGL((k_step<NP, NS, true, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, in,
+                       snap, last, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_step<NP, NS, false, EPL>), dim3(grid), dim3(kBlock), 0, st, in, out,
-                       out2, p->d_scale, a);
+    hipLaunchKernelGGL((k_step<NP, NS, false, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, in,
+                       snap, last, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-template <int NP, int NS, int EPL>
-int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double* usnap,
-                 double* eta, double t_next, double dt, double src, hipStream_t st) {
-  AdjArgs<NP> a;
+template <int NP, int NS, int EPL, int MS>
+int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double* snap,
+                 double* eta, const double* t_next, const double* src, double dt,
+                 hipStream_t st) {
+  AdjArgs<NP, MS> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
   a.sc = dt;
-  a.uin_res = inflow_value(p, t_next);
-  a.src = src;
+  for (int m = 0; m < MS; ++m) {
+    a.uin_res[m] = inflow_value(p, t_next[m]);
+    a.src[m] = src[m];
+  }
   a.ktot = p->ktot;
+  a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr;
-  constexpr int TE = kBlock * EPL - 2 * NS;
+  constexpr int TE = kBlock * EPL - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_adj<NP, NS, true, EPL>), dim3(grid), dim3(kBlock), 0, st, win, wout,
-                       usnap, eta, p->d_scale, a);
+    hipLaunchKernelGGL((k_adj<NP, NS, true, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, win,
+                       wout, snap, eta, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_adj<NP, NS, false, EPL>), dim3(grid), dim3(kBlock), 0, st, win, wout,
-                       usnap, eta, p->d_scale, a);
+    hipLaunchKernelGGL((k_adj<NP, NS, false, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, win,
+                       wout, snap, eta, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
+// Instantiated shapes: (elements per lane, steps per launch) in {(1,1), (2,1), (1,2), (1,4)};
+// 4 steps per launch only for Np <= 8 (at Np = 9 hipcc/ROCm 7.2 fails instruction
+// selection for that shape; chunk() never asks for it there).
 template <int NP, int NS>
-int launch_step_t(const dg_plan* p, const double* in, double* out, double* out2, double t,
-                  double dt, hipStream_t st) {
-  // 4 elements per lane is instantiated for Np <= 5 only (register budget; larger Np
-  // use 2).
-  switch (p->epl) {
-    case 1: return launch_step_e<NP, NS, 1>(p, in, out, out2, t, dt, st);
-    case 4:
-      if constexpr (NP <= 5) return launch_step_e<NP, NS, 4>(p, in, out, out2, t, dt, st);
-      [[fallthrough]];
-    default: return launch_step_e<NP, NS, 2>(p, in, out, out2, t, dt, st);
-  }
+int launch_step_t(const dg_plan* p, int ms, const double* in, double* snap, double* last,
+                  const double* times, double dt, hipStream_t st) {
+  if constexpr (NP <= 8)
+    if (ms == 4) return launch_step_e<NP, NS, 1, 4>(p, in, snap, last, times, dt, st);
+  if (ms == 2) return launch_step_e<NP, NS, 1, 2>(p, in, snap, last, times, dt, st);
+  if (p->epl == 2) return launch_step_e<NP, NS, 2, 1>(p, in, snap, last, times, dt, st);
+  return launch_step_e<NP, NS, 1, 1>(p, in, snap, last, times, dt, st);
 }
 
 template <int NP, int NS>
-int launch_adj_t(const dg_plan* p, const double* win, double* wout, const double* usnap,
-                 double* eta, double t_next, double dt, double src, hipStream_t st) {
-  switch (p->epl) {
-    case 1: return launch_adj_e<NP, NS, 1>(p, win, wout, usnap, eta, t_next, dt, src, st);
-    case 4:
-      if constexpr (NP <= 5)
-        return launch_adj_e<NP, NS, 4>(p, win, wout, usnap, eta, t_next, dt, src, st);
-      [[fallthrough]];
-    default: return launch_adj_e<NP, NS, 2>(p, win, wout, usnap, eta, t_next, dt, src, st);
-  }
+int launch_adj_t(const dg_plan* p, int ms, const double* win, double* wout, const double* snap,
+                 double* eta, const double* t_next, const double* src, double dt,
+                 hipStream_t st) {
+  if constexpr (NP <= 8)
+    if (ms == 4) return launch_adj_e<NP, NS, 1, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
+  if (ms == 2) return launch_adj_e<NP, NS, 1, 2>(p, win, wout, snap, eta, t_next, src, dt, st);
+  if (p->epl == 2)
+    return launch_adj_e<NP, NS, 2, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
+  return launch_adj_e<NP, NS, 1, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
 }
 
 // Dispatch on Np (2..9) and the number of stages.
@@ -1009,26 +1046,36 @@ int launch_adj_t(const dg_plan* p, const double* win, double* wout, const double
     default: return fail(DG_ERR_ARG, "unsupported Np"); \
   }
 
-int launch_step(const dg_plan* p, const double* in, double* out, double* out2, double t,
-                double dt, hipStream_t st) {
+int launch_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
+                const double* times, double dt, hipStream_t st) {
   int rc = DG_OK;
   if (p->nstages == 5) {
-    DG_DISPATCH_NP(p->NP, rc = (launch_step_t<NP, 5>(p, in, out, out2, t, dt, st)));
+    DG_DISPATCH_NP(p->NP, rc = (launch_step_t<NP, 5>(p, ms, in, snap, last, times, dt, st)));
   } else {
-    DG_DISPATCH_NP(p->NP, rc = (launch_step_t<NP, 1>(p, in, out, out2, t, dt, st)));
+    DG_DISPATCH_NP(p->NP, rc = (launch_step_t<NP, 1>(p, ms, in, snap, last, times, dt, st)));
   }
   return rc;
 }
 
-int launch_adj(const dg_plan* p, const double* win, double* wout, const double* usnap,
-               double* eta, double t_next, double dt, double src, hipStream_t st) {
+int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const double* snap,
+               double* eta, const double* t_next, const double* src, double dt, hipStream_t st) {
   int rc = DG_OK;
   if (p->nstages == 5) {
-    DG_DISPATCH_NP(p->NP, rc = (launch_adj_t<NP, 5>(p, win, wout, usnap, eta, t_next, dt, src, st)));
+    DG_DISPATCH_NP(p->NP,
+                   rc = (launch_adj_t<NP, 5>(p, ms, win, wout, snap, eta, t_next, src, dt, st)));
   } else {
-    DG_DISPATCH_NP(p->NP, rc = (launch_adj_t<NP, 1>(p, win, wout, usnap, eta, t_next, dt, src, st)));
+    DG_DISPATCH_NP(p->NP,
+                   rc = (launch_adj_t<NP, 1>(p, ms, win, wout, snap, eta, t_next, src, dt, st)));
   }
   return rc;
+}
+
+// Steps per launch for the next chunk of `left` steps (greedy over {4, 2, 1}, capped by
+// the plan's setting).
+inline int chunk(const dg_plan* p, int left) {
+  int m = (p->NP > 8 && p->msteps > 2) ? 2 : p->msteps;
+  while (m > left) m >>= 1;
+  return m < 1 ? 1 : m;
 }
 
 }  // namespace
@@ -1102,7 +1149,11 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   {
     if (const char* v = std::getenv("DG_ELEMS_PER_LANE")) {
       const int k = std::atoi(v);
-      if (k == 1 || k == 2 || k == 4) p->epl = k;
+      if (k == 1 || k == 2) p->epl = k;
+    }
+    if (const char* v = std::getenv("DG_STEPS_PER_LAUNCH")) {
+      const int k = std::atoi(v);
+      if (k == 1 || k == 2 || k == 4) p->msteps = k;
     }
   }
   auto cleanup = [&](const std::string& m) {
@@ -1113,6 +1164,8 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   if (hipMalloc(&p->d_VX, sizeof(double) * (K + 1)) != hipSuccess) return cleanup("hipMalloc VX");
   if (hipMalloc(&p->d_scratch, sizeof(double) * p->ktot * NP) != hipSuccess)
     return cleanup("hipMalloc scratch");
+  if (hipMalloc(&p->d_scratch2, sizeof(double) * p->ktot * NP) != hipSuccess)
+    return cleanup("hipMalloc scratch2");
   if (hipMalloc(&p->d_pv, sizeof(double) * kArgmaxParts) != hipSuccess) return cleanup("hipMalloc pv");
   if (hipMalloc(&p->d_pi, sizeof(int64_t) * kArgmaxParts) != hipSuccess) return cleanup("hipMalloc pi");
   if (hipMemcpy(p->d_scale, scale.data(), sizeof(double) * K, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1129,13 +1182,14 @@ int dg_plan_destroy(dg_plan* p) {
   if (p->d_scale) (void)hipFree(p->d_scale);
   if (p->d_VX) (void)hipFree(p->d_VX);
   if (p->d_scratch) (void)hipFree(p->d_scratch);
+  if (p->d_scratch2) (void)hipFree(p->d_scratch2);
   if (p->d_pv) (void)hipFree(p->d_pv);
   if (p->d_pi) (void)hipFree(p->d_pi);
   delete p;
   return DG_OK;
 }
 
-int dg_plan_query(const dg_plan* p, int64_t out[6]) {
+int dg_plan_query(const dg_plan* p, int64_t out[8]) {
   if (!p || !out) return fail(DG_ERR_ARG, "null argument");
   out[0] = p->N;
   out[1] = p->NP;
@@ -1143,6 +1197,8 @@ int dg_plan_query(const dg_plan* p, int64_t out[6]) {
   out[3] = p->batch;
   out[4] = p->uniform ? 1 : 0;
   out[5] = p->nstages;
+  out[6] = p->epl;
+  out[7] = (p->NP > 8 && p->msteps > 2) ? 2 : p->msteps;
   return DG_OK;
 }
 
@@ -1150,9 +1206,13 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
   if (!p) return fail(DG_ERR_ARG, "null plan");
   switch (key) {
     case DG_TUNE_ELEMS_PER_LANE:
-      if (value != 1 && value != 2 && value != 4)
-        return fail(DG_ERR_ARG, "elements per lane must be 1, 2 or 4");
+      if (value != 1 && value != 2) return fail(DG_ERR_ARG, "elements per lane must be 1 or 2");
       p->epl = int(value);
+      return DG_OK;
+    case DG_TUNE_STEPS_PER_LAUNCH:
+      if (value != 1 && value != 2 && value != 4)
+        return fail(DG_ERR_ARG, "steps per launch must be 1, 2 or 4");
+      p->msteps = int(value);
       return DG_OK;
     default:
       return fail(DG_ERR_ARG, "unknown tuning key");
@@ -1179,33 +1239,39 @@ int dg_lserk4_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, doubl
   if (nsteps == 0) return DG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t field = p->ktot * p->NP;
-  double time = t0;  // time = time + dt, as One_code.mlx:139
+  // Time levels by repeated addition (time = time + dt, One_code.mlx:139).
+  std::vector<double> tn(size_t(nsteps) + 1);
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
   if (snapshots) {
     if (snapshots != u)
       HIP_TRY(hipMemcpyAsync(snapshots, u, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
-    for (int n = 0; n < nsteps; ++n) {
-      double* out2 = (n == nsteps - 1 && snapshots != u) ? u : nullptr;
-      const int rc = launch_step(p, snapshots + int64_t(n) * field,
-                                 snapshots + int64_t(n + 1) * field, out2, time, dt, st);
+    for (int n = 0; n < nsteps;) {
+      const int m = chunk(p, nsteps - n);
+      double* last = (n + m == nsteps && snapshots != u) ? u : nullptr;
+      const int rc = launch_step(p, m, snapshots + int64_t(n) * field,
+                                 snapshots + int64_t(n + 1) * field, last, &tn[n], dt, st);
       if (rc) return rc;
-      time = time + dt;
+      n += m;
     }
     return DG_OK;
   }
-  // Ping-pong between u and the plan scratch; the last step lands in u.
-  // Step n writes b then swaps, so the last write lands in u when the first source
-  // is u for even nsteps and the scratch copy of u for odd nsteps.
+  // Ping-pong between u and the plan scratch; if the launch count is odd the first launch
+  // reads a scratch copy of u so that the last one lands in u.
+  int launches = 0;
+  for (int n = 0; n < nsteps; n += chunk(p, nsteps - n)) ++launches;
   double* a = u;
   double* b = p->d_scratch;
-  if (nsteps % 2 == 1) {
+  if (launches % 2 == 1) {
     HIP_TRY(hipMemcpyAsync(b, a, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
-    std::swap(a, b);  // a = scratch (holds u^0), b = u
+    std::swap(a, b);
   }
-  for (int n = 0; n < nsteps; ++n) {
-    const int rc = launch_step(p, a, b, nullptr, time, dt, st);
+  for (int n = 0; n < nsteps;) {
+    const int m = chunk(p, nsteps - n);
+    const int rc = launch_step(p, m, a, nullptr, b, &tn[n], dt, st);
     if (rc) return rc;
     std::swap(a, b);
-    time = time + dt;
+    n += m;
   }
   return DG_OK;
 }
@@ -1217,23 +1283,33 @@ int dg_lserk4_adj(dg_plan* p, double* w, const double* snapshots, double t0, dou
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t field = p->ktot * p->NP;
   // Same time levels as the forward sweep (repeated addition).
-  std::vector<double> tn(size_t(nsteps) + 1);
+  std::vector<double> tn(size_t(nsteps) + 1), src(size_t(nsteps) + 1, src_coef);
   tn[0] = t0;
   for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
-  double* a = w;
-  double* b = p->d_scratch;
-  for (int n = nsteps - 1; n >= 0; --n) {
-    const double src = (n == nsteps - 1) ? 0.0 : src_coef;
-    const int rc = launch_adj(p, a, b, snapshots + int64_t(n + 1) * field, eta, tn[n + 1], dt,
-                              src, st);
+  src[nsteps] = 0.0;  // left-endpoint rule: no source at the terminal node
+  // Launch l reads buf[l] and writes buf[l+1]: buf[0] = w, the last output = w, and the
+  // intermediate states alternate between the two plan scratch fields.  (w may alias the
+  // terminal snapshot: only the first launch reads snapshot nsteps.)
+  int launches = 0;
+  for (int n = nsteps; n > 0; n -= chunk(p, n)) ++launches;
+  int l = 0;
+  const double* in = w;
+  for (int n = nsteps; n > 0; ++l) {  // this launch covers steps n-m .. n-1
+    const int m = chunk(p, n);
+    const int n0 = n - m;
+    // (a single launch cannot write its own input: it goes through scratch and back)
+    double* out = (l == launches - 1 && launches > 1)
+                      ? w : ((l % 2 == 0) ? p->d_scratch : p->d_scratch2);
+    const int rc = launch_adj(p, m, in, out, snapshots + int64_t(n0 + 1) * field, eta,
+                              &tn[n0 + 1], &src[n0 + 1], dt, st);
     if (rc) return rc;
-    std::swap(a, b);
+    in = out;
+    n = n0;
   }
-  // Node-0 source and the hand-back into w.
-  if (src_coef != 0.0 || a != w) {
-    const double c = (nsteps > 0) ? src_coef : 0.0;
-    hipLaunchKernelGGL(k_axpy_copy, dim3(grid_for(field, kBlock)), dim3(kBlock), 0, st, a,
-                       snapshots, c, w, field);
+  // Node-0 source K^0 = src * u^0 (and the hand-back of a single-launch sweep).
+  if ((src_coef != 0.0 && nsteps > 0) || in != w) {
+    hipLaunchKernelGGL(k_axpy_copy, dim3(grid_for(field, kBlock)), dim3(kBlock), 0, st, in,
+                       snapshots, nsteps > 0 ? src_coef : 0.0, w, field);
     HIP_TRY(hipGetLastError());
   }
   return DG_OK;

@@ -55,9 +55,12 @@ class EnsembleSweep:
     self.snaps = self.op.new_field(self.nsteps + 1)
     # u^0 lives in snapshot 0; the forward sweep with u aliasing it leaves it untouched.
     self.op.init_sine(amp, freq, phase, out=self.snaps[0])
-    self.w = self.op.new_field()
+    # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
+    # place on snapshot N (the library allows that alias) and leaves dJ/du^0 there.
+    self.w = self.snaps[self.nsteps]
     self.eta = torch.zeros(self.op.ktot, dtype=torch.float64, device=self.op.device)
     self.partial = torch.zeros(self.op.K, dtype=torch.float64, device=self.op.device)
+    self._graphs = None
 
   @property
   def dof_updates(self):
@@ -68,9 +71,35 @@ class EnsembleSweep:
     self.op.forward(self.snaps[0], 0.0, self.dt, self.nsteps, self.snaps)
 
   def adjoint(self):
-    self.w.copy_(self.snaps[self.nsteps])
     self.eta.zero_()
     self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta)
+
+  def capture(self):
+    """Capture the forward and adjoint sweeps as two HIP graphs (replayed by
+    forward_graph / adjoint_graph): the per-launch host work (operator constants, inflow
+    values) is baked in once and the kernels run back to back."""
+    dev = self.op.device
+    torch.cuda.synchronize(dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):  # warm-up outside capture
+      self.forward()
+      self.adjoint()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    gf, ga = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gf):
+      self.forward()
+    with torch.cuda.graph(ga):
+      self.adjoint()
+    self._graphs = (gf, ga)
+    return self
+
+  def forward_graph(self):
+    self._graphs[0].replay()
+
+  def adjoint_graph(self):
+    self._graphs[1].replay()
 
   def reduce(self):
     sum_rows(self.eta, self.batch, out=self.partial)

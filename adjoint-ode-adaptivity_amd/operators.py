@@ -73,11 +73,16 @@ class DGAdvection1D:
     _lib.check(rc, "dg_plan_create")
     self._plan = handle
     self._lib = lib
-    q = (ctypes.c_int64 * 6)()
-    _lib.check(lib.dg_plan_query(self._plan, q), "dg_plan_query")
+    self._query()
+    self._idx = torch.zeros(1, dtype=torch.int64, device=self.device)
+
+  def _query(self):
+    q = (ctypes.c_int64 * 8)()
+    _lib.check(self._lib.dg_plan_query(self._plan, q), "dg_plan_query")
     self.uniform = bool(q[4])
     self.stages = int(q[5])
-    self._idx = torch.zeros(1, dtype=torch.int64, device=self.device)
+    self.elems_per_lane = int(q[6])
+    self.steps_per_launch = int(q[7])
 
   # --- lifetime ---
   def close(self):
@@ -97,12 +102,17 @@ class DGAdvection1D:
   def __exit__(self, *exc):
     self.close()
 
-  def tune(self, elems_per_lane=None):
+  def tune(self, elems_per_lane=None, steps_per_launch=None):
     """Shape of the fused step kernels (results are bit-identical for every setting):
-    each lane holds ``elems_per_lane`` elements (1, 2 or 4; tile = 256 * that)."""
+    each lane holds ``elems_per_lane`` elements (1 or 2; single-step launches), and
+    ``steps_per_launch`` (1, 2 or 4) time steps are fused per launch."""
     if elems_per_lane is not None:
       _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_ELEMS_PER_LANE,
                                         int(elems_per_lane)), "dg_plan_tune")
+    if steps_per_launch is not None:
+      _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_STEPS_PER_LAUNCH,
+                                        int(steps_per_launch)), "dg_plan_tune")
+    self._query()
     return self
 
   # --- checks ---

@@ -37,7 +37,8 @@ def parse():
   p.add_argument("--K", type=int, default=1 << 20)
   p.add_argument("--nsteps", type=int, default=20, help="time steps per sweep (each direction)")
   p.add_argument("--no-cpu-baseline", action="store_true")
-  p.add_argument("--cpu-steps", type=int, default=6, help="time steps of the CPU sample")
+  p.add_argument("--cpu-steps", type=int, default=12, help="time steps of the CPU sample")
+  p.add_argument("--eager", action="store_true", help="launch the sweeps eagerly (no HIP graph)")
   return p.parse_args()
 
 
@@ -91,19 +92,18 @@ def main():
     params = ens.ic_params([rank])
   sweep = ens.EnsembleSweep(mesh, [rank], nsteps, dt, params=params)
   reducer = ens.DeviceReducer(sweep.op)
+  if not args.eager:
+    sweep.capture()  # each sweep becomes one HIP graph launch
   stream = torch.cuda.current_stream(dev)
 
   def one_step(ev=None):
     if ev:
       ev[0].record(stream)
-    sweep.forward()
+    sweep.forward() if args.eager else sweep.forward_graph()
     if ev:
       ev[1].record(stream)
-    sweep.w.copy_(sweep.snaps[nsteps])
-    sweep.eta.zero_()
-    if ev:
       ev[2].record(stream)
-    sweep.op.adjoint(sweep.w, sweep.snaps, 0.0, dt, nsteps, eta=sweep.eta)
+    sweep.adjoint() if args.eager else sweep.adjoint_graph()
     if ev:
       ev[3].record(stream)
     partial = sweep.reduce()
@@ -134,12 +134,23 @@ def main():
   fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
   adj_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
   Np, ktot = N + 1, K
-  fwd_launch_us = fwd_ms * 1e3 / nsteps
-  adj_launch_us = adj_ms * 1e3 / nsteps
-  # Algorithmic bytes per launch: forward 16 B/DOF (read u^n, write
-  # u^{n+1}); adjoint 24 B/DOF (read w^{n+1}, read u^{n+1}, write w^n) + 16 B/element (eta rmw).
-  fwd_bytes = 16.0 * Np * ktot
-  adj_bytes = 24.0 * Np * ktot + 16.0 * ktot
+  ms = sweep.op.steps_per_launch
+  launches = 0
+  left = nsteps
+  while left > 0:  # the library's greedy chunking of a sweep into launches
+    m = ms
+    while m > left:
+      m //= 2
+    left -= m
+    launches += 1
+  fwd_launch_us = fwd_ms * 1e3 / launches
+  adj_launch_us = adj_ms * 1e3 / launches
+  # Algorithmic bytes per launch of `ms` fused steps:
+  #   forward: read u^n once, write the ms snapshots u^{n+1..n+ms}:  (8 + 8 ms) B per DOF
+  #   adjoint: read w^{n+ms}, read the ms snapshots, write w^n: (16 + 8 ms) B per DOF,
+  #            plus the indicator read-modify-write, 16 B per element.
+  fwd_bytes = (8.0 + 8.0 * ms) * Np * ktot
+  adj_bytes = (16.0 + 8.0 * ms) * Np * ktot + 16.0 * ktot
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = None
@@ -148,7 +159,7 @@ def main():
     try:
       with open(PROFILE_TRAFFIC) as f:
         tr = json.load(f)
-      if tr.get("N") == N and tr.get("K") == K:
+      if tr.get("N") == N and tr.get("K") == K and tr.get("steps_per_launch") == ms:
         traffic = tr.get("adj_bytes_per_launch")
         traffic_src = tr.get("source")
     except (OSError, ValueError):
@@ -156,6 +167,10 @@ def main():
 
   total_dofs = sweep.dof_updates * world * args.steps
   value = total_dofs / elapsed
+  # The single-step algorithm moves 16 B (fwd) + 24 B + 16/Np B (adj) per pair of
+  # DOF-updates, so its HBM roofline is 8 TB/s / that per-update average.
+  single_step_bytes = (16.0 + 24.0 + 16.0 / Np) / 2.0
+  single_step_roofline = HBM_PEAK_GBS * 1e9 / single_step_bytes * world
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
       "value": value,
@@ -175,12 +190,17 @@ def main():
                  "parallelism": f"ensemble-dp{world}"},
       "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                   "kernel": "k_adj<5,5,true> (adjoint step + DWR)",
+                   "kernel": f"k_adj<{Np},5,uniform,1,{ms}> ({ms} reverse steps + DWR per launch)",
                    "launch_us": adj_launch_us, "algorithmic_bytes": adj_bytes,
                    "traffic_source": traffic_src},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": fwd_gbs / HBM_PEAK_GBS, "kernel": "k_step<5,5,true>",
+                       "frac": fwd_gbs / HBM_PEAK_GBS,
+                       "kernel": f"k_step<{Np},5,uniform,1,{ms}> ({ms} steps per launch)",
                        "launch_us": fwd_launch_us, "algorithmic_bytes": fwd_bytes},
+      "single_step_roofline": {"value": single_step_roofline, "unit": "DOF-updates/s",
+                               "bytes_per_update": single_step_bytes,
+                               "frac": value / single_step_roofline},
+      "steps_per_launch": ms,
       "refine_index": ref_idx,
   }
   if rank == 0 and world == 1 and not args.no_cpu_baseline:

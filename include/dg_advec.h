@@ -73,13 +73,17 @@ int dg_plan_create(int N, int64_t K, int64_t batch,
 int dg_plan_destroy(dg_plan* plan);
 
 /* Query plan sizes: out[0]=N, out[1]=Np, out[2]=K, out[3]=batch, out[4]=uniform mesh (0/1),
- * out[5]=time stages per step. */
-int dg_plan_query(const dg_plan* plan, int64_t out[6]);
+ * out[5]=time stages per step, out[6]=elements per lane, out[7]=time steps per launch. */
+int dg_plan_query(const dg_plan* plan, int64_t out[8]);
 
-/* Tuning knob of the fused step kernels (results are bit-identical for every setting).
- *   DG_TUNE_ELEMS_PER_LANE  elements held per lane: 1, 2 or 4 (tile = 256*value elements)
- * Environment override at plan creation: DG_ELEMS_PER_LANE. */
-enum { DG_TUNE_ELEMS_PER_LANE = 1 };
+/* Tuning knobs of the fused step kernels (results are bit-identical for every setting).
+ *   DG_TUNE_ELEMS_PER_LANE    elements held per lane: 1 or 2 (tile = 256*value elements);
+ *                             2 applies to single-step launches only
+ *   DG_TUNE_STEPS_PER_LAUNCH  time steps fused per launch: 1, 2 or 4 (temporal blocking:
+ *                             each launch reads its input state once and writes every
+ *                             intermediate snapshot; halo = steps*stages elements per side)
+ * Environment overrides at plan creation: DG_ELEMS_PER_LANE, DG_STEPS_PER_LAUNCH. */
+enum { DG_TUNE_ELEMS_PER_LANE = 1, DG_TUNE_STEPS_PER_LAUNCH = 2 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* rhs = AdvecRHS1D(u, t, a)   — utils/AdvecRHS1D.m:1-20 (inline copy One_code.mlx:124-134).
@@ -102,7 +106,9 @@ int dg_lserk4_fwd(dg_plan* plan, double* u, double t0, double dt, int nsteps,
  *              R = LIFT*(Fscale.*du): the interelement-jump (strong-form) residual of AdvecRHS1D
  *   w^n      = S^T w^{n+1}
  * and finally w^0 += src_coef * u^0.
- *   w (in/out): terminal dJ/du^N on entry, dJ/du^0 on exit.
+ *   w (in/out): terminal dJ/du^N on entry, dJ/du^0 on exit.  w may alias the terminal
+ *               snapshot (snapshots + nsteps*field, i.e. J = |u^N|^2/2); that snapshot is
+ *               then overwritten.
  *   snapshots : the (nsteps+1) forward states written by dg_lserk4_fwd.
  *   eta (nullable): batch*K accumulators (caller zeroes them). */
 int dg_lserk4_adj(dg_plan* plan, double* w, const double* snapshots, double t0, double dt,

@@ -22,7 +22,7 @@ def main():
   p.add_argument("--K", type=int, default=1 << 20)
   p.add_argument("--nsteps", type=int, default=20)
   p.add_argument("--rounds", type=int, default=5)
-  p.add_argument("--variants", default="1,2,4")
+  p.add_argument("--variants", default="1:1,2:1,1:2,1:4")
   a = p.parse_args()
   pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
   mesh = pkg.BaseGalerkin1D(n=a.N, k=a.K)
@@ -32,12 +32,12 @@ def main():
   op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
   w = op.new_field()
   eta = torch.zeros(op.ktot, dtype=torch.float64, device=op.device)
-  variants = [int(v) for v in a.variants.split(",")]
+  variants = [tuple(int(x) for x in v.split(":")) for v in a.variants.split(",")]
   res = {v: {"fwd": [], "adj": []} for v in variants}
   st = torch.cuda.current_stream()
   for r in range(a.rounds + 1):
     for v in variants:
-      op.tune(elems_per_lane=v)
+      op.tune(elems_per_lane=v[0], steps_per_launch=v[1])
       e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
       e[0].record(st)
       op.forward(snaps[0], 0.0, dt, a.nsteps, snaps)
@@ -54,7 +54,7 @@ def main():
   out = {}
   for v in variants:
     f, d = float(np.median(res[v]["fwd"])), float(np.median(res[v]["adj"]))
-    out[f"elems_per_lane={v}"] = {"fwd_us": f, "fwd_GBs": fb / f / 1e3, "adj_us": d,
+    out[f"epl={v[0]} steps/launch={v[1]}"] = {"fwd_us": f, "fwd_GBs": fb / f / 1e3, "adj_us": d,
                                          "adj_GBs": ab / d / 1e3,
                                          "fwd_min_us": float(np.min(res[v]["fwd"])),
                                          "adj_min_us": float(np.min(res[v]["adj"]))}
