@@ -36,6 +36,9 @@ def parse():
   p.add_argument("--N", type=int, default=4)
   p.add_argument("--K", type=int, default=1 << 20)
   p.add_argument("--nsteps", type=int, default=20, help="time steps per sweep (each direction)")
+  p.add_argument("--ics", type=int, default=0,
+                 help="ensemble size over all ranks (config 4: --K 65536 --ics 1024); "
+                      "default: one trajectory per rank (config 2 per GPU, weak scaling)")
   p.add_argument("--no-cpu-baseline", action="store_true")
   p.add_argument("--cpu-steps", type=int, default=12, help="time steps of the CPU sample")
   p.add_argument("--eager", action="store_true", help="launch the sweeps eagerly (no HIP graph)")
@@ -86,11 +89,16 @@ def main():
   N, K, nsteps = args.N, args.K, args.nsteps
   mesh = pkg.BaseGalerkin1D(n=N, k=K, domain=[0.0, 1.0])
   dt = mesh.cfl_dt()
-  if rank == 0:
-    params = (np.array([1.0]), np.array([1.0]), np.array([0.0]))  # sin(2 pi x)
-  else:
-    params = ens.ic_params([rank])
-  sweep = ens.EnsembleSweep(mesh, [rank], nsteps, dt, params=params)
+  if args.ics > 0:  # config 4: the ensemble is sharded over the ranks (strong scaling)
+    ics = list(ens.shard(args.ics, rank, world))
+    params = ens.ic_params(ics)
+    n_total = args.ics
+  else:  # one trajectory per rank (weak scaling); rank 0 runs the golden IC
+    ics = [rank]
+    params = ((np.array([1.0]), np.array([1.0]), np.array([0.0])) if rank == 0
+              else ens.ic_params([rank]))
+    n_total = world
+  sweep = ens.EnsembleSweep(mesh, ics, nsteps, dt, params=params)
   reducer = ens.DeviceReducer(sweep.op)
   if not args.eager:
     sweep.capture()  # each sweep becomes one HIP graph launch
@@ -107,7 +115,7 @@ def main():
     if ev:
       ev[3].record(stream)
     partial = sweep.reduce()
-    _, idx = ens.gather_indicator(partial, world, reducer)
+    _, idx = ens.gather_indicator(partial, n_total, reducer)
     return int(idx.item())  # the refine index goes to the host (mesh split)
 
   for _ in range(args.warmup):
@@ -133,7 +141,7 @@ def main():
 
   fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
   adj_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
-  Np, ktot = N + 1, K
+  Np, ktot = N + 1, K * sweep.batch
   ms = sweep.op.steps_per_launch
   launches = 0
   left = nsteps
@@ -165,7 +173,12 @@ def main():
     except (OSError, ValueError):
       pass
 
-  total_dofs = sweep.dof_updates * world * args.steps
+  if world > 1:
+    d = torch.tensor([float(sweep.dof_updates)], dtype=torch.float64, device=dev)
+    dist.all_reduce(d)
+    total_dofs = float(d.item()) * args.steps
+  else:
+    total_dofs = sweep.dof_updates * args.steps
   value = total_dofs / elapsed
   # The single-step algorithm moves 16 B (fwd) + 24 B + 16/Np B (adj) per pair of
   # DOF-updates, so its HBM roofline is 8 TB/s / that per-update average.
@@ -180,14 +193,15 @@ def main():
       "warmup": args.warmup,
       "ms_per_step": elapsed / args.steps * 1e3,
       "higher_is_better": True,
-      "scaling": "weak",
+      "scaling": "strong" if args.ics > 0 else "weak",
       "vs_baseline": None,
       "dtype": "f64",
       "data": "synthetic (u0 = sin(2 pi x) on rank 0, SURVEY 8d sine-family ICs on other ranks)",
-      "config": {"workload": f"config 2: 1D DG advection N={N} K={K} LSERK4 fwd+adj "
-                             f"{nsteps}+{nsteps} steps/sweep + DWR indicator + refine argmax",
-                 "N": N, "K": K, "nsteps_per_sweep": nsteps, "trajectories_per_gpu": 1,
-                 "parallelism": f"ensemble-dp{world}"},
+      "config": {"workload": (f"config {'4' if args.ics > 0 else '2'}: 1D DG advection N={N} "
+                              f"K={K} x {n_total} trajectories, LSERK4 fwd+adj {nsteps}+{nsteps} "
+                              f"steps/sweep + DWR indicator + refine argmax"),
+                 "N": N, "K": K, "nsteps_per_sweep": nsteps, "trajectories": n_total,
+                 "trajectories_per_gpu": sweep.batch, "parallelism": f"ensemble-dp{world}"},
       "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
                    "kernel": f"k_adj<{Np},5,uniform,1,{ms}> ({ms} reverse steps + DWR per launch)",
@@ -203,7 +217,7 @@ def main():
       "steps_per_launch": ms,
       "refine_index": ref_idx,
   }
-  if rank == 0 and world == 1 and not args.no_cpu_baseline:
+  if rank == 0 and world == 1 and args.ics == 0 and not args.no_cpu_baseline:
     out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_steps)
   if rank == 0:
     print(json.dumps(out), flush=True)

@@ -393,3 +393,40 @@ def test_ensemble_sweep_graph_matches_eager(pkg, gpu):
   torch.cuda.synchronize()
   np.testing.assert_array_equal(host(pa), host(pb))
   np.testing.assert_array_equal(host(a.w), host(b.w))
+
+
+def test_dg_adapt_loop_refines_the_oracle_argmax(pkg, gpu):
+  """The DG adapt loop (factory.DGFunFactory): GPU sweeps + indicator + argmax split,
+  against the oracle indicator computed from the same snapshots; the refine index must
+  agree whenever the oracle's top-2 gap exceeds the parity tolerance."""
+  import torch
+  fac = pkg.factory
+  problem = fac.DGProblem(N=3, nsteps=12)
+  afuns = fac.DGFunFactory(problem).getAdaptFunctions()
+  v_x = np.linspace(0.0, 1.0, 41)
+  state = fac.DGAdaptState(problem, v_x)
+  u0_fn = lambda x: np.sin(2 * np.pi * x) + 0.5 * np.exp(-200 * (x - 0.3) ** 2)  # noqa: E731
+  seen = []
+  for _ in range(4):
+    v_x_now = np.asarray(state.times_new)
+    state = afuns.adapt(state, u0_fn)
+    # oracle on the same mesh (GPU forward snapshots as inputs)
+    S = setup1d.startup1d(3, v_x_now, metric="element")
+    mesh = pkg.BaseGalerkin1D(n=3, v_x=v_x_now)
+    op = make_op(pkg, mesh)
+    dt = mesh.cfl_dt()
+    snaps = op.new_field(problem.nsteps + 1)
+    snaps[0].copy_(dev(mesh.to_device_layout(u0_fn(mesh.x)), gpu))
+    op.forward(snaps[0], 0.0, dt, problem.nsteps, snaps)
+    gs = [setup1d.from_elem_major(host(snaps[n]), 4) for n in range(problem.nsteps + 1)]
+    times = [0.0]
+    for _n in range(problem.nsteps):
+      times.append(times[-1] + dt)
+    _, eta_ref, _ = oadj.adjoint_sweep(gs[-1], gs, times, dt, A, S)
+    assert rel_err(state.err_steps, np.abs(eta_ref)) <= RTOL
+    top = np.sort(np.abs(eta_ref))[::-1]
+    if top[0] - top[1] > 1e-8 * top[0]:
+      assert state.ref_idx == int(np.argmax(np.abs(eta_ref)))
+    assert len(state.times_new) == len(v_x_now) + 1
+    seen.append(state.ref_idx)
+  assert len(state.times_new) == 45  # four splits of a 40-element mesh
