@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -117,6 +118,7 @@ template <int NP, int NS, int MS> struct StepArgs {
   int64_t ktot;         // batch * K elements
   int64_t stride;       // doubles between consecutive snapshots
   int32_t K;            // elements per trajectory
+  int32_t xcd;          // XCD-aware tile order (speed only)
 };
 
 template <int NP, int MS> struct AdjArgs {
@@ -128,6 +130,7 @@ template <int NP, int MS> struct AdjArgs {
   int64_t stride;      // doubles between consecutive snapshots
   int32_t K;
   int32_t has_eta;
+  int32_t xcd;         // XCD-aware tile order (speed only)
 };
 
 // ---------------------------------------------------------------------------
@@ -182,7 +185,7 @@ template <int NP, int EPL> struct TileRegs {
   int off;
 };
 
-template <int NP, int EPL>
+template <int NP, int EPL, bool EDGE = true>
 __device__ __forceinline__ void tile_issue(const double* __restrict__ g, int64_t e0, int64_t nd,
                                            TileRegs<NP, EPL>& r) {
   using G = TileGeo<NP, EPL>;
@@ -197,7 +200,7 @@ __device__ __forceinline__ void tile_issue(const double* __restrict__ g, int64_t
     const int64_t gd = base + 2 * int64_t(v);
     double2 val = make_double2(0.0, 0.0);
     if (v < nvec) {
-      if (gd >= 0 && gd + 1 < nd) {
+      if (!EDGE || (gd >= 0 && gd + 1 < nd)) {  // interior tiles: always in range
         val = g2[gd >> 1];
       } else {
         if (gd >= 0 && gd < nd) val.x = g[gd];
@@ -234,6 +237,29 @@ __device__ __forceinline__ void store_run(double* __restrict__ g, int64_t o0, in
   }
 }
 
+// Store a full tile output (COUNT doubles, compile-time) from lds to g[o0..); o0 even.
+template <int COUNT>
+__device__ __forceinline__ void store_full(double* __restrict__ g, int64_t o0,
+                                           const double* __restrict__ lds) {
+  static_assert(COUNT % 2 == 0, "16-byte runs");
+  constexpr int NV = COUNT / 2, NQ = (NV + kBlock - 1) / kBlock;
+  double2* __restrict__ g2 = reinterpret_cast<double2*>(g + o0);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int v = int(threadIdx.x) + q * kBlock;
+    if ((q + 1) * kBlock <= NV || v < NV) g2[v] = *reinterpret_cast<const double2*>(&lds[2 * v]);
+  }
+}
+
+// A tile is an edge tile when its element range [e0, e0+T) leaves [0, ktot) or contains
+// a trajectory's first or last element (uniform per workgroup).  Interior tiles -- all
+// but a handful -- run a specialisation without inflow/outflow selects or bounds checks.
+__device__ __forceinline__ bool edge_tile(int64_t e0, int T, int64_t ktot, int32_t K) {
+  if (e0 < 0 || e0 + T > ktot) return true;
+  const int64_t kl0 = int64_t(uint32_t(e0) % uint32_t(K));
+  return kl0 == 0 || kl0 + T >= K;
+}
+
 // Per-element geometry: global element e = e0 + el, position kl inside its trajectory.
 struct Elem {
   int64_t e;
@@ -241,10 +267,17 @@ struct Elem {
   bool inrange, first, last, valid;
 };
 
-template <int H, int T>
+template <int H, int T, bool EDGE = true>
 __device__ __forceinline__ Elem elem_info(int64_t e0, int el, int64_t ktot, int32_t K) {
   Elem E;
   E.e = e0 + el;
+  if constexpr (!EDGE) {
+    E.kl = int32_t(uint32_t(E.e) % uint32_t(K));
+    E.inrange = true;
+    E.first = E.last = false;
+    E.valid = el >= H && el < T - H;
+    return E;
+  }
   E.inrange = (E.e >= 0 && E.e < ktot);
   // ktot < 2^31 (checked at plan creation): 32-bit division.
   E.kl = E.inrange ? int32_t(uint32_t(E.e) % uint32_t(K)) : 0;
@@ -253,6 +286,27 @@ __device__ __forceinline__ Elem elem_info(int64_t e0, int el, int64_t ktot, int3
   E.valid = E.inrange && el >= H && el < T - H;
   return E;
 }
+
+// Tile of workgroup b.  The dispatcher deals workgroups round-robin over the 8 XCDs
+// (b, b+8, ... share one; cdna_hip_programming.md §5.5 T1), so giving each XCD a
+// contiguous range of tiles makes neighbouring tiles -- which re-read each other's halo
+// lines -- run on one L2.  Bijective for any n; a speed choice only.
+__device__ __forceinline__ int64_t tile_of(int64_t b, int64_t n, bool xcd) {
+  if (!xcd || n < 16) return b;
+  const int64_t q = n / 8, r = n % 8, x = b % 8, j = b / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
+
+// Boundary handling in the face exchange is done by *index* selection into LDS (one
+// 32-bit v_cndmask), never by value/pointer selection: `c ? kernarg : lds[i]` lets the
+// compiler fold a select of pointers into a flat load on every stage's critical path.
+// Each kernel keeps its per-stage boundary constants (inflow values, a zero) in a few
+// doubles at the end of its LDS array, written by edge tiles only.
+
+// Materialise a value at this point of the program: an empty volatile asm keeps its
+// order with the barrier, so work placed before a __syncthreads() is not sunk below it by
+// the IR optimisers (the machine scheduler never moves code across s_barrier).
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
 
 // Even/odd element state helpers.
 template <int NP>
@@ -311,30 +365,39 @@ __device__ __forceinline__ void stage_out(double* __restrict__ lds, const double
 // snap + st*stride (if snap) and after the last step also to `last` (if non-null).
 // UNI: the operator constants already carry dt*2/h.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int EPL, int MS>
-__global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
-                                                 double* __restrict__ snap,
-                                                 double* __restrict__ last,
-                                                 const double* __restrict__ scale,
-                                                 StepArgs<NP, NS, MS> args) {
+template <int NP, int NS, bool UNI, int EPL, int MS, bool EDGE>
+__device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile,
+                                          const double* __restrict__ uin,
+                                          double* __restrict__ snap, double* __restrict__ last,
+                                          const double* __restrict__ scale,
+                                          const StepArgs<NP, NS, MS>& args) {
   using G = TileGeo<NP, EPL>;
   constexpr int T = G::T;
   constexpr int H = MS * NS;     // dependency cone: one element per stage
   constexpr int TE = T - 2 * H;  // output elements per tile (even)
   static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
-  __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int lane = threadIdx.x;
-  const int64_t tile = blockIdx.x;
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
   const int64_t o0 = tile * TE * NP;
   const int64_t rem = nd - o0;
   const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
 
+  constexpr int CB = G::kLds;  // lds[CB + st*NS + s] = inflow value of that stage
   TileRegs<NP, EPL> pf;
-  tile_issue<NP, EPL>(uin, e0, nd, pf);
+  tile_issue<NP, EPL, EDGE>(uin, e0, nd, pf);
   tile_commit<NP, EPL>(pf, lds);
+  if constexpr (EDGE) {
+    // Lane-indexed read straight from the kernel-argument segment (k_step's args follow
+    // its 4 pointer arguments): read as a uniform struct member, the compiler hoists these
+    // 2*MS*NS SGPRs over the whole kernel and pushes the interior path into SGPR spills.
+    using SArgs = StepArgs<NP, NS, MS>;
+    const double* ka = reinterpret_cast<const double*>(
+        static_cast<const char*>(__builtin_amdgcn_kernarg_segment_ptr()) + 4 * sizeof(void*) +
+        offsetof(SArgs, uin));
+    if (lane < MS * NS) lds[CB + lane] = ka[lane];
+  }
   __syncthreads();
   double ev[EPL][NE], od[EPL][NO];  // the element state in even/odd coordinates
   Elem E[EPL];
@@ -343,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
   for (int m = 0; m < EPL; ++m) {
     const int el = m * kBlock + lane;
     to_eo<NP>(lds + pf.off + el * NP, ev[m], od[m]);
-    E[m] = elem_info<H, T>(e0, el, args.ktot, args.K);
+    E[m] = elem_info<H, T, EDGE>(e0, el, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
   }
@@ -357,6 +420,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
       const int fL = (s & 1) * 2 * (T + 2);  // faceL = lds[fL ...], faceR = lds[fR ...]
       const int fR = fL + (T + 2);
       double u0[EPL], uN[EPL];
+      double pe[EPL][NE], po[EPL][NO];
 #pragma unroll
       for (int m = 0; m < EPL; ++m) {
         const int el = m * kBlock + lane;
@@ -364,6 +428,30 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
         uN[m] = ev[m][0] - od[m][0];
         lds[fL + el + 1] = u0[m];
         lds[fR + el + 1] = uN[m];
+        __builtin_amdgcn_sched_barrier(0);  // face writes first, then hide their latency:
+        // Everything that does not need the neighbours' faces is issued before the barrier
+        // (s_barrier is a scheduling boundary): the volume term and, on uniform meshes,
+        // the low-storage carry A_s*r.  Only the lift term and the update follow it.
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          double t = (UNI && s > 0) ? RK<NS>::A(s) * re[m][k] : args.op.Qeo[k * NO] * od[m][0];
+#pragma unroll
+          for (int j = (UNI && s > 0) ? 0 : 1; j < NO; ++j)
+            t = fma(args.op.Qeo[k * NO + j], od[m][j], t);
+          pe[m][k] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          double t = (UNI && s > 0) ? RK<NS>::A(s) * ro[m][k] : args.op.Qoe[k * NE] * ev[m][0];
+#pragma unroll
+          for (int j = (UNI && s > 0) ? 0 : 1; j < NE; ++j)
+            t = fma(args.op.Qoe[k * NE + j], ev[m][j], t);
+          po[m][k] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pin(pe[m][k]);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) pin(po[m][k]);
       }
       __syncthreads();
 #pragma unroll
@@ -371,34 +459,31 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
         const int el = m * kBlock + lane;
         // faceR[el] is element el-1's right node, faceL[el+2] element el+1's left node; the
         // pad entries are only read by the outermost halo elements, whose results are dropped.
-        const double uL = E[m].first ? args.uin[st * NS + s] : lds[fR + el];
-        const double uR = lds[fL + el + 2];
-        const double du0 = u0[m] - uL;
-        const double du1 = E[m].last ? 0.0 : (uN[m] - uR);
+        // Interior tiles: neighbours' faces.  Edge tiles: the first element of a
+        // trajectory reads the inflow value, the last one its own right face (du1 = 0).
+        const int iL = EDGE && E[m].first ? CB + st * NS + s : fR + el;
+        const int iR = EDGE && E[m].last ? fR + el + 1 : fL + el + 2;
+        const double du0 = u0[m] - lds[iL];
+        const double du1 = uN[m] - lds[iR];
         const double dlt = du0 - du1, sig = du0 + du1;
-        double ae[NE], ao[NO];
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
-          double t = args.op.le[k] * dlt;
-#pragma unroll
-          for (int j = 0; j < NO; ++j) t = fma(args.op.Qeo[k * NO + j], od[m][j], t);
-          ae[k] = UNI ? t : sc[m] * t;
-        }
-#pragma unroll
-        for (int k = 0; k < NO; ++k) {
-          double t = args.op.lo[k] * sig;
-#pragma unroll
-          for (int j = 0; j < NE; ++j) t = fma(args.op.Qoe[k * NE + j], ev[m][j], t);
-          ao[k] = UNI ? t : sc[m] * t;
-        }
-#pragma unroll
-        for (int k = 0; k < NE; ++k) {
-          re[m][k] = (s == 0) ? ae[k] : fma(RK<NS>::A(s), re[m][k], ae[k]);  // rk4a(1) = 0
+          if constexpr (UNI) {  // r = A_s r + dt*L u, dt*2/h folded into the operator
+            re[m][k] = fma(args.op.le[k], dlt, pe[m][k]);
+          } else {
+            const double a = sc[m] * fma(args.op.le[k], dlt, pe[m][k]);
+            re[m][k] = (s == 0) ? a : fma(RK<NS>::A(s), re[m][k], a);  // rk4a(1) = 0
+          }
           ev[m][k] = fma(RK<NS>::B(s), re[m][k], ev[m][k]);
         }
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
-          ro[m][k] = (s == 0) ? ao[k] : fma(RK<NS>::A(s), ro[m][k], ao[k]);
+          if constexpr (UNI) {
+            ro[m][k] = fma(args.op.lo[k], sig, po[m][k]);
+          } else {
+            const double a = sc[m] * fma(args.op.lo[k], sig, po[m][k]);
+            ro[m][k] = (s == 0) ? a : fma(RK<NS>::A(s), ro[m][k], a);
+          }
           od[m][k] = fma(RK<NS>::B(s), ro[m][k], od[m][k]);
         }
       }
@@ -407,11 +492,32 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
       __syncthreads();  // the last stage's face reads are done before the image is rewritten
       stage_out<NP, EPL, H>(lds, ev, od, false);
       __syncthreads();
-      if (snap != nullptr) store_run(snap + st * args.stride, o0, count, lds);
-      if (st == MS - 1 && last != nullptr) store_run(last, o0, count, lds);
+      if constexpr (EDGE) {
+        if (snap != nullptr) store_run(snap + st * args.stride, o0, count, lds);
+        if (st == MS - 1 && last != nullptr) store_run(last, o0, count, lds);
+      } else {
+        if (snap != nullptr) store_full<TE * NP>(snap + st * args.stride, o0, lds);
+        if (st == MS - 1 && last != nullptr) store_full<TE * NP>(last, o0, lds);
+      }
       if (st < MS - 1) __syncthreads();  // the next stage's faces alias the image
     }
   }
+}
+
+template <int NP, int NS, bool UNI, int EPL, int MS>
+__global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
+                                                 double* __restrict__ snap,
+                                                 double* __restrict__ last,
+                                                 const double* __restrict__ scale,
+                                                 StepArgs<NP, NS, MS> args) {
+  using G = TileGeo<NP, EPL>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * NS];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
+  if (edge_tile(e0, G::T, args.ktot, args.K))
+    step_tile<NP, NS, UNI, EPL, MS, true>(lds, tile, uin, snap, last, scale, args);
+  else
+    step_tile<NP, NS, UNI, EPL, MS, false>(lds, tile, uin, snap, last, scale, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -424,29 +530,37 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
 // Indicator: eta += dt * sum_i w_i * s*(L0_i du0 + L1_i du1), with L0.w = le.we + lo.wo and
 // L1.w = -le.we + lo.wo.  The next snapshot tile is prefetched during each step's stages.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int EPL, int MS>
-__global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
-                                                double* __restrict__ wout,
-                                                const double* __restrict__ snap,
-                                                double* __restrict__ eta,
-                                                const double* __restrict__ scale,
-                                                AdjArgs<NP, MS> args) {
+template <int NP, int NS, bool UNI, int EPL, int MS, bool EDGE>
+__device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
+                                         const double* __restrict__ win,
+                                         double* __restrict__ wout,
+                                         const double* __restrict__ snap,
+                                         double* __restrict__ eta,
+                                         const double* __restrict__ scale,
+                                         const AdjArgs<NP, MS>& args) {
   using G = TileGeo<NP, EPL>;
   constexpr int T = G::T;
   constexpr int H = MS * NS;
   constexpr int TE = T - 2 * H;
   static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
-  __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int lane = threadIdx.x;
-  const int64_t tile = blockIdx.x;
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
+  constexpr int CB = G::kLds;  // lds[CB + st] = inflow value at t_{n+st+1}; lds[CB + MS] = 0
   TileRegs<NP, EPL> pw, pu;
-  tile_issue<NP, EPL>(win, e0, nd, pw);
-  tile_issue<NP, EPL>(snap + (MS - 1) * args.stride, e0, nd, pu);
+  tile_issue<NP, EPL, EDGE>(win, e0, nd, pw);
+  tile_issue<NP, EPL, EDGE>(snap + (MS - 1) * args.stride, e0, nd, pu);
   tile_commit<NP, EPL>(pw, lds);
+  if constexpr (EDGE) {
+    using AArgs = AdjArgs<NP, MS>;
+    const double* ka = reinterpret_cast<const double*>(  // see step_tile; 5 pointer args
+        static_cast<const char*>(__builtin_amdgcn_kernarg_segment_ptr()) + 5 * sizeof(void*) +
+        offsetof(AArgs, uin_res));
+    if (lane < MS) lds[CB + lane] = ka[lane];
+    if (lane == MS) lds[CB + MS] = 0.0;
+  }
   __syncthreads();
   double we[EPL][NE], wo[EPL][NO];
 #pragma unroll
@@ -465,7 +579,7 @@ __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
   double eacc[EPL];
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
-    E[m] = elem_info<H, T>(e0, m * kBlock + lane, args.ktot, args.K);
+    E[m] = elem_info<H, T, EDGE>(e0, m * kBlock + lane, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
     eacc[m] = 0.0;
@@ -477,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
     tile_commit<NP, EPL>(pu, lds);
     const int off = pu.off;
     __syncthreads();
-    if (st > 0) tile_issue<NP, EPL>(snap + (st - 1) * args.stride, e0, nd, pu);
+    if (st > 0) tile_issue<NP, EPL, EDGE>(snap + (st - 1) * args.stride, e0, nd, pu);
 #pragma unroll
     for (int m = 0; m < EPL; ++m) {
       const int el = m * kBlock + lane;
@@ -492,10 +606,17 @@ __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
       }
       if (args.has_eta) {
         // Neighbour face values of the snapshot for the jump residual.
-        const double usL = (el > 0) ? lds[off + (el - 1) * NP + (NP - 1)] : us[0];
-        const double usR = (el < T - 1) ? lds[off + (el + 1) * NP] : us[NP - 1];
-        const double du0 = us[0] - (E[m].first ? args.uin_res[st] : usL);
-        const double du1 = E[m].last ? 0.0 : (us[NP - 1] - usR);
+        // Lane 0 / lane T-1 read their own end node (in range; halo results are dropped).
+        // Edge tiles: a trajectory's first element reads the inflow value, its last
+        // element its own right node (du1 = 0).
+        int iL = off + (el > 0 ? (el - 1) * NP + (NP - 1) : 0);
+        int iR = off + (el < T - 1 ? (el + 1) * NP : el * NP + NP - 1);
+        if constexpr (EDGE) {
+          iL = E[m].first ? CB + st : iL;
+          iR = E[m].last ? off + el * NP + NP - 1 : iR;
+        }
+        const double du0 = us[0] - lds[iL];
+        const double du1 = us[NP - 1] - lds[iR];
         double pe = 0.0, po = 0.0;
 #pragma unroll
         for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[m][k], pe);
@@ -541,18 +662,13 @@ __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
         }
         // adjoints of du0 and du1 (du0 - du1 feeds the even part, du0 + du1 the odd part)
         g0[m] = gd + gs;
-        g1[m] = E[m].last ? 0.0 : (gs - gd);
+        g1[m] = gs - gd;
+        if constexpr (EDGE) g1[m] = E[m].last ? 0.0 : g1[m];
         lds[f0 + el + 1] = g0[m];
         lds[f1 + el + 1] = g1[m];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int m = 0; m < EPL; ++m) {
-        const int el = m * kBlock + lane;
-        // du0 = u_0 - (left neighbour's u_N); du1 = u_N - (right neighbour's u_0), with
-        // u_0 = e_0 + o_0 and u_N = e_0 - o_0.
-        const double gl = E[m].first ? 0.0 : lds[f1 + el];     // g1 of element k-1
-        const double gr = E[m].last ? 0.0 : lds[f0 + el + 2];  // g0 of element k+1
+        __builtin_amdgcn_sched_barrier(0);  // face writes first
+        // The transposed volume term and the carry A_s*lr need no neighbour data: issued
+        // before the barrier (a scheduling boundary), only the face terms follow it.
 #pragma unroll
         for (int j = 0; j < NE; ++j) {
           double t = we[m][j];
@@ -567,12 +683,26 @@ __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
           for (int k = 0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[m][k], t);
           wo[m][j] = t;
         }
-        we[m][0] += (g0[m] + g1[m]) - (gr + gl);
-        wo[m][0] += (g0[m] - g1[m]) + (gr - gl);
 #pragma unroll
         for (int k = 0; k < NE; ++k) le_[m][k] = RK<NS>::A(s) * le_[m][k];
 #pragma unroll
         for (int k = 0; k < NO; ++k) lo_[m][k] = RK<NS>::A(s) * lo_[m][k];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pin(we[m][k]);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) pin(wo[m][k]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < EPL; ++m) {
+        const int el = m * kBlock + lane;
+        // du0 = u_0 - (left neighbour's u_N); du1 = u_N - (right neighbour's u_0), with
+        // u_0 = e_0 + o_0 and u_N = e_0 - o_0.
+        // g1 of element k-1 and g0 of element k+1 (edge tiles: zero across trajectory ends)
+        const double gl = lds[EDGE && E[m].first ? CB + MS : f1 + el];
+        const double gr = lds[EDGE && E[m].last ? CB + MS : f0 + el + 2];
+        we[m][0] += (g0[m] + g1[m]) - (gr + gl);
+        wo[m][0] += (g0[m] - g1[m]) + (gr - gl);
       }
     }
   }
@@ -584,9 +714,29 @@ __global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
   stage_out<NP, EPL, H>(lds, we, wo, true);
   __syncthreads();
   const int64_t o0 = tile * TE * NP;
-  const int64_t rem = nd - o0;
-  const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
-  store_run(wout, o0, count, lds);
+  if constexpr (EDGE) {
+    const int64_t rem = nd - o0;
+    store_run(wout, o0, rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP, lds);
+  } else {
+    store_full<TE * NP>(wout, o0, lds);
+  }
+}
+
+template <int NP, int NS, bool UNI, int EPL, int MS>
+__global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
+                                                double* __restrict__ wout,
+                                                const double* __restrict__ snap,
+                                                double* __restrict__ eta,
+                                                const double* __restrict__ scale,
+                                                AdjArgs<NP, MS> args) {
+  using G = TileGeo<NP, EPL>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS + 1];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
+  if (edge_tile(e0, G::T, args.ktot, args.K))
+    adj_tile<NP, NS, UNI, EPL, MS, true>(lds, tile, win, wout, snap, eta, scale, args);
+  else
+    adj_tile<NP, NS, UNI, EPL, MS, false>(lds, tile, win, wout, snap, eta, scale, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -861,6 +1011,7 @@ struct dg_plan {
   // tuning (dg_plan_tune): elements per lane of the step kernels (tile = 256*epl elements)
   int epl = 1;
   int msteps = 4;  // time steps fused per launch (1, 2 or 4)
+  int xcd_order = 1;  // XCD-aware tile order
 };
 
 namespace {
@@ -968,6 +1119,7 @@ int launch_step_e(const dg_plan* p, const double* in, double* snap, double* last
   a.ktot = p->ktot;
   a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
+  a.xcd = p->xcd_order;
   constexpr int TE = kBlock * EPL - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
@@ -995,6 +1147,7 @@ int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double
   a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr;
+  a.xcd = p->xcd_order;
   constexpr int TE = kBlock * EPL - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
@@ -1007,14 +1160,20 @@ int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double
   return DG_OK;
 }
 
-// Instantiated shapes: (elements per lane, steps per launch) in {(1,1), (2,1), (1,2), (1,4)};
+// Instantiated shapes: (elements per lane, steps per launch) in {(1,1), (2,1), (1,2), (1,4)},
+// plus (2,2), (2,4) for Np <= 6;
 // 4 steps per launch only for Np <= 8 (at Np = 9 hipcc/ROCm 7.2 fails instruction
 // selection for that shape; chunk() never asks for it there).
 template <int NP, int NS>
 int launch_step_t(const dg_plan* p, int ms, const double* in, double* snap, double* last,
                   const double* times, double dt, hipStream_t st) {
-  if constexpr (NP <= 8)
+  if constexpr (NP <= 8) {
+    if (ms == 4 && p->epl == 2 && NP <= 6)
+      return launch_step_e<NP, NS, 2, 4>(p, in, snap, last, times, dt, st);
     if (ms == 4) return launch_step_e<NP, NS, 1, 4>(p, in, snap, last, times, dt, st);
+  }
+  if (ms == 2 && p->epl == 2 && NP <= 6)
+    return launch_step_e<NP, NS, 2, 2>(p, in, snap, last, times, dt, st);
   if (ms == 2) return launch_step_e<NP, NS, 1, 2>(p, in, snap, last, times, dt, st);
   if (p->epl == 2) return launch_step_e<NP, NS, 2, 1>(p, in, snap, last, times, dt, st);
   return launch_step_e<NP, NS, 1, 1>(p, in, snap, last, times, dt, st);
@@ -1024,8 +1183,13 @@ template <int NP, int NS>
 int launch_adj_t(const dg_plan* p, int ms, const double* win, double* wout, const double* snap,
                  double* eta, const double* t_next, const double* src, double dt,
                  hipStream_t st) {
-  if constexpr (NP <= 8)
+  if constexpr (NP <= 8) {
+    if (ms == 4 && p->epl == 2 && NP <= 6)
+      return launch_adj_e<NP, NS, 2, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
     if (ms == 4) return launch_adj_e<NP, NS, 1, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
+  }
+  if (ms == 2 && p->epl == 2 && NP <= 6)
+    return launch_adj_e<NP, NS, 2, 2>(p, win, wout, snap, eta, t_next, src, dt, st);
   if (ms == 2) return launch_adj_e<NP, NS, 1, 2>(p, win, wout, snap, eta, t_next, src, dt, st);
   if (p->epl == 2)
     return launch_adj_e<NP, NS, 2, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
@@ -1208,6 +1372,9 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
     case DG_TUNE_ELEMS_PER_LANE:
       if (value != 1 && value != 2) return fail(DG_ERR_ARG, "elements per lane must be 1 or 2");
       p->epl = int(value);
+      return DG_OK;
+    case DG_TUNE_XCD_ORDER:
+      p->xcd_order = value ? 1 : 0;
       return DG_OK;
     case DG_TUNE_STEPS_PER_LAUNCH:
       if (value != 1 && value != 2 && value != 4)

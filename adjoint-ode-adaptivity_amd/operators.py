@@ -102,10 +102,15 @@ class DGAdvection1D:
   def __exit__(self, *exc):
     self.close()
 
-  def tune(self, elems_per_lane=None, steps_per_launch=None):
-    """Shape of the fused step kernels (results are bit-identical for every setting):
-    each lane holds ``elems_per_lane`` elements (1 or 2; single-step launches), and
-    ``steps_per_launch`` (1, 2 or 4) time steps are fused per launch."""
+  def tune(self, elems_per_lane=None, steps_per_launch=None, xcd_order=None):
+    """Shape of the fused step kernels: each lane holds ``elems_per_lane`` elements (1 or
+    2), ``steps_per_launch`` (1, 2 or 4) time steps are fused per launch, and
+    ``xcd_order`` gives each XCD a contiguous range of tiles.  Elements per lane and the
+    tile order do not change the arithmetic; steps per launch changes it at rounding
+    level (the state stays in even/odd coordinates between fused steps)."""
+    if xcd_order is not None:
+      _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_XCD_ORDER, int(xcd_order)),
+                 "dg_plan_tune")
     if elems_per_lane is not None:
       _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_ELEMS_PER_LANE,
                                         int(elems_per_lane)), "dg_plan_tune")

@@ -77,13 +77,14 @@ int dg_plan_destroy(dg_plan* plan);
 int dg_plan_query(const dg_plan* plan, int64_t out[8]);
 
 /* Tuning knobs of the fused step kernels (results are bit-identical for every setting).
- *   DG_TUNE_ELEMS_PER_LANE    elements held per lane: 1 or 2 (tile = 256*value elements);
- *                             2 applies to single-step launches only
+ *   DG_TUNE_ELEMS_PER_LANE    elements held per lane: 1 or 2 (tile = 256*value elements;
+ *                             2 with 2 or 4 steps per launch needs Np <= 6)
  *   DG_TUNE_STEPS_PER_LAUNCH  time steps fused per launch: 1, 2 or 4 (temporal blocking:
  *                             each launch reads its input state once and writes every
  *                             intermediate snapshot; halo = steps*stages elements per side)
+ *   DG_TUNE_XCD_ORDER         0/1: give each XCD a contiguous range of tiles (speed only)
  * Environment overrides at plan creation: DG_ELEMS_PER_LANE, DG_STEPS_PER_LAUNCH. */
-enum { DG_TUNE_ELEMS_PER_LANE = 1, DG_TUNE_STEPS_PER_LAUNCH = 2 };
+enum { DG_TUNE_ELEMS_PER_LANE = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* rhs = AdvecRHS1D(u, t, a)   — utils/AdvecRHS1D.m:1-20 (inline copy One_code.mlx:124-134).

@@ -1,7 +1,15 @@
-# SQ/GRBM counter passes for the step kernels (one pass per counter group; no tracing).
+# SQ/GRBM counter passes for one step kernel (one pass per counter group; no tracing).
+#   bash profiles/collect_sq.sh <tag> [fwd_nosnap|fwd|adj]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-TAG=${1:-r1}
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/sq_a_$TAG" -- python3 "$GRAFT_REPO_ROOT/profiles/ab_variants.py" --variants 1:4 --rounds 1 --nsteps 20 > gpurun_out/sq_a_$TAG.log 2>&1 || { echo "pass A failed"; tail -20 gpurun_out/sq_a_$TAG.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/sq_b_$TAG" -- python3 "$GRAFT_REPO_ROOT/profiles/ab_variants.py" --variants 1:4 --rounds 1 --nsteps 20 > gpurun_out/sq_b_$TAG.log 2>&1 || { echo "pass B failed"; tail -20 gpurun_out/sq_b_$TAG.log; exit 1; }
+TAG=${1:-r1}; WHAT=${2:-fwd_nosnap}
+timeout -k 10 120 rocprofv3 -L > gpurun_out/counters_avail.txt 2>&1 || true
+i=0
+for G in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+         "SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SALU" \
+         "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+         "SQ_LEVEL_WAVES SQ_ACCUM_PREV_HIRES SQ_BUSY_CU_CYCLES SQ_INST_LEVEL_LDS SQ_INSTS_BRANCH"; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --pmc $G --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/sq_${TAG}_$i" -- python3 "$GRAFT_REPO_ROOT/profiles/kernel_driver.py" --what $WHAT > gpurun_out/sq_${TAG}_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/sq_${TAG}_$i.log; }
+done
 echo done

@@ -1,0 +1,50 @@
+"""Minimal driver for counter collection on one step kernel (no timing, no checks):
+
+  python profiles/kernel_driver.py --what fwd_nosnap|fwd|adj [--N 4] [--K 1048576] [--reps 3]
+
+Runs `reps` sweeps of 20 steps of the chosen kernel after one warm-up sweep."""
+import argparse
+import importlib
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+  p = argparse.ArgumentParser()
+  p.add_argument("--what", default="fwd_nosnap")
+  p.add_argument("--N", type=int, default=4)
+  p.add_argument("--K", type=int, default=1 << 20)
+  p.add_argument("--nsteps", type=int, default=20)
+  p.add_argument("--reps", type=int, default=3)
+  p.add_argument("--steps-per-launch", type=int, default=4)
+  a = p.parse_args()
+  pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
+  mesh = pkg.BaseGalerkin1D(n=a.N, k=a.K)
+  op = pkg.operators.DGAdvection1D(mesh).tune(steps_per_launch=a.steps_per_launch)
+  dt = mesh.cfl_dt()
+  snaps = op.new_field(a.nsteps + 1)
+  op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
+  op.forward(snaps[0], 0.0, dt, a.nsteps, snaps)
+  w = op.new_field()
+  eta = torch.zeros(op.ktot, dtype=torch.float64, device=op.device)
+  u = op.new_field()
+  for _ in range(a.reps + 1):
+    if a.what == "fwd_nosnap":
+      u.copy_(snaps[0])
+      op.forward(u, 0.0, dt, a.nsteps)
+    elif a.what == "fwd":
+      op.forward(snaps[0], 0.0, dt, a.nsteps, snaps)
+    else:
+      w.copy_(snaps[a.nsteps])
+      op.adjoint(w, snaps, 0.0, dt, a.nsteps, eta=eta)
+  torch.cuda.synchronize()
+  print("ok", a.what)
+
+
+if __name__ == "__main__":
+  main()

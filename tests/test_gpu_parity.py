@@ -336,9 +336,9 @@ def test_kernel_variants_bit_identical(pkg, gpu, N, K):
   dt = oadv.bench_dt(S)
   outs = []
   nsteps = 7  # exercises the greedy 4 + 2 + 1 chunking
-  shapes = ((1, 1), (2, 1), (1, 2), (1, 4))
-  for epl, ms in shapes:
-    op = make_op(pkg, mesh).tune(elems_per_lane=epl, steps_per_launch=ms)
+  shapes = ((1, 1, 1), (2, 1, 0), (1, 2, 1), (1, 4, 1), (2, 4, 0), (1, 4, 0), (2, 2, 1))
+  for epl, ms, xcd in shapes:
+    op = make_op(pkg, mesh).tune(elems_per_lane=epl, steps_per_launch=ms, xcd_order=xcd)
     snaps = op.new_field(nsteps + 1)
     op.forward(u0.clone(), 0.0, dt, nsteps, snaps)
     w = snaps[nsteps].clone()
@@ -352,6 +352,9 @@ def test_kernel_variants_bit_identical(pkg, gpu, N, K):
   # step), so different steps-per-launch agree to rounding.
   for a_, b_ in zip(outs[0], outs[1]):
     np.testing.assert_array_equal(a_, b_)
+  for i, j in ((3, 4), (3, 5)):  # same steps per launch, other lane packing / tile order
+    for a_, b_ in zip(outs[i], outs[j]):
+      np.testing.assert_array_equal(a_, b_)
   # States agree to 1e-12; the indicator (a cancellation-limited jump residual) to RTOL.
   for o in outs[2:]:
     for a_, b_, tol in zip(outs[0], o, (1e-12, 1e-12, RTOL, 1e-12)):
