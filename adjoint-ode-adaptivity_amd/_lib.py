@@ -15,7 +15,7 @@ HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "include", "dg_advec.h"
 DG_OK, DG_ERR_ARG, DG_ERR_HIP, DG_ERR_NOMEM = 0, -1, -2, -3
 DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T = 0, 1
 DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
-DG_TUNE_ELEMS_PER_LANE, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
+DG_TUNE_TILE_WIDTH, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
 
 _c_dbl_p = ctypes.POINTER(ctypes.c_double)
 _vp = ctypes.c_void_p

@@ -162,17 +162,16 @@ __device__ __forceinline__ int load_tile(const double* __restrict__ g, int64_t e
 
 
 // ---------------------------------------------------------------------------
-// Tile geometry of the fused step kernels.  A workgroup of kBlock lanes owns a tile of
-// T = kBlock*EPL consecutive elements; lane l holds elements l, l+kBlock, ... (EPL of
-// them) in VGPRs.  The dependency cone of one step is NS elements per side, so the
-// TE = T - 2*NS interior elements are exact and written back.  EPL > 1 puts more bytes
-// in flight per resident wave (the kernels are co-limited by HBM and fp64 VALU, and one
-// 256-element tile per workgroup does not hold enough loads in flight to cover HBM
-// latency at the residency their 106 SGPRs allow).
+// Tile geometry of the fused step kernels.  A workgroup of LB = 256*W lanes owns a tile
+// of T = LB consecutive elements, one element per lane, its state in VGPRs.  The
+// dependency cone of one step is NS elements per side, so of MS fused steps the
+// TE = T - 2*MS*NS interior elements are exact and written back.  W = 2 halves the
+// redundant halo work (the kernels are fp64-VALU bound) at the same registers per lane.
 // ---------------------------------------------------------------------------
-template <int NP, int EPL> struct TileGeo {
-  static constexpr int T = kBlock * EPL;
-  static constexpr int kVec = (T * NP + 2 + 2 * kBlock - 1) / (2 * kBlock);  // double2 / lane
+template <int NP, int W> struct TileGeo {
+  static constexpr int LB = kBlock * W;
+  static constexpr int T = LB;
+  static constexpr int kVec = (T * NP + 2 + 2 * LB - 1) / (2 * LB);  // double2 / lane
   static constexpr int kTileD = T * NP + 2;  // staging image (+2: 16-byte realignment)
   static constexpr int kFaceD = 4 * (T + 2);  // 2 double-buffered face arrays, padded by 1
   static constexpr int kLds = kTileD > kFaceD ? kTileD : kFaceD;
@@ -180,15 +179,15 @@ template <int NP, int EPL> struct TileGeo {
 
 // Issue the 16-byte loads of one tile image into registers (coalesced: lane-consecutive
 // double2), then commit them to LDS.  Elements outside [0, ktot) read as zero.
-template <int NP, int EPL> struct TileRegs {
-  double2 v[TileGeo<NP, EPL>::kVec];
+template <int NP, int W> struct TileRegs {
+  double2 v[TileGeo<NP, W>::kVec];
   int off;
 };
 
-template <int NP, int EPL, bool EDGE = true>
+template <int NP, int W, bool EDGE = true>
 __device__ __forceinline__ void tile_issue(const double* __restrict__ g, int64_t e0, int64_t nd,
-                                           TileRegs<NP, EPL>& r) {
-  using G = TileGeo<NP, EPL>;
+                                           TileRegs<NP, W>& r) {
+  using G = TileGeo<NP, W>;
   const int64_t d0 = e0 * NP;
   const int64_t base = d0 & ~int64_t(1);
   r.off = int(d0 - base);
@@ -196,7 +195,7 @@ __device__ __forceinline__ void tile_issue(const double* __restrict__ g, int64_t
   const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
 #pragma unroll
   for (int q = 0; q < G::kVec; ++q) {
-    const int v = threadIdx.x + q * kBlock;
+    const int v = threadIdx.x + q * G::LB;
     const int64_t gd = base + 2 * int64_t(v);
     double2 val = make_double2(0.0, 0.0);
     if (v < nvec) {
@@ -211,22 +210,23 @@ __device__ __forceinline__ void tile_issue(const double* __restrict__ g, int64_t
   }
 }
 
-template <int NP, int EPL>
-__device__ __forceinline__ void tile_commit(const TileRegs<NP, EPL>& r, double* __restrict__ lds) {
-  using G = TileGeo<NP, EPL>;
+template <int NP, int W>
+__device__ __forceinline__ void tile_commit(const TileRegs<NP, W>& r, double* __restrict__ lds) {
+  using G = TileGeo<NP, W>;
   const int nvec = (G::T * NP + r.off + 1) >> 1;
 #pragma unroll
   for (int q = 0; q < G::kVec; ++q) {
-    const int v = threadIdx.x + q * kBlock;
+    const int v = threadIdx.x + q * G::LB;
     if (v < nvec) *reinterpret_cast<double2*>(&lds[2 * v]) = r.v[q];
   }
 }
 
 // Store `count` doubles from lds[0..count) to g[o0..o0+count); o0 must be even.
+template <int LB = kBlock>
 __device__ __forceinline__ void store_run(double* __restrict__ g, int64_t o0, int64_t count,
                                           const double* __restrict__ lds) {
   double2* __restrict__ g2 = reinterpret_cast<double2*>(g);
-  for (int64_t v = threadIdx.x; 2 * v < count; v += kBlock) {
+  for (int64_t v = threadIdx.x; 2 * v < count; v += LB) {
     const double2 val = *reinterpret_cast<const double2*>(&lds[2 * v]);
     const int64_t gd = o0 + 2 * v;
     if (2 * v + 1 < count) {
@@ -238,16 +238,16 @@ __device__ __forceinline__ void store_run(double* __restrict__ g, int64_t o0, in
 }
 
 // Store a full tile output (COUNT doubles, compile-time) from lds to g[o0..); o0 even.
-template <int COUNT>
+template <int COUNT, int LB>
 __device__ __forceinline__ void store_full(double* __restrict__ g, int64_t o0,
                                            const double* __restrict__ lds) {
   static_assert(COUNT % 2 == 0, "16-byte runs");
-  constexpr int NV = COUNT / 2, NQ = (NV + kBlock - 1) / kBlock;
+  constexpr int NV = COUNT / 2, NQ = (NV + LB - 1) / LB;
   double2* __restrict__ g2 = reinterpret_cast<double2*>(g + o0);
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    const int v = int(threadIdx.x) + q * kBlock;
-    if ((q + 1) * kBlock <= NV || v < NV) g2[v] = *reinterpret_cast<const double2*>(&lds[2 * v]);
+    const int v = int(threadIdx.x) + q * LB;
+    if ((q + 1) * LB <= NV || v < NV) g2[v] = *reinterpret_cast<const double2*>(&lds[2 * v]);
   }
 }
 
@@ -334,15 +334,15 @@ __device__ __forceinline__ void from_eo(const double* ev, const double* od, doub
 // Write the TE interior elements of the tile (element-major, nodal) through the LDS
 // image with 16-byte stores.  Callers barrier before (face reads done) and after (when
 // the image is reused).
-template <int NP, int EPL, int H>
+template <int NP, int W, int H>
 __device__ __forceinline__ void stage_out(double* __restrict__ lds, const double (*ev)[(NP + 1) / 2],
                                           const double (*od)[NP / 2], bool dual) {
-  constexpr int T = kBlock * EPL;
+  constexpr int T = TileGeo<NP, W>::T, EPL = 1;
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   const int lane = threadIdx.x;
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
-    const int el = m * kBlock + lane;
+    const int el = m * T + lane;
     if (el >= H && el < T - H) {
       double* o = lds + (el - H) * NP;
       if (dual) {  // dual coordinates back to nodal: w_k = (we+wo)/2, w_{N-k} = (we-wo)/2
@@ -365,14 +365,14 @@ __device__ __forceinline__ void stage_out(double* __restrict__ lds, const double
 // snap + st*stride (if snap) and after the last step also to `last` (if non-null).
 // UNI: the operator constants already carry dt*2/h.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int EPL, int MS, bool EDGE>
+template <int NP, int NS, bool UNI, int W, int MS, bool EDGE>
 __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile,
                                           const double* __restrict__ uin,
                                           double* __restrict__ snap, double* __restrict__ last,
                                           const double* __restrict__ scale,
                                           const StepArgs<NP, NS, MS>& args) {
-  using G = TileGeo<NP, EPL>;
-  constexpr int T = G::T;
+  using G = TileGeo<NP, W>;
+  constexpr int T = G::T, LB = G::LB, EPL = 1;
   constexpr int H = MS * NS;     // dependency cone: one element per stage
   constexpr int TE = T - 2 * H;  // output elements per tile (even)
   static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
@@ -385,16 +385,16 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
   const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
 
   constexpr int CB = G::kLds;  // lds[CB + st*NS + s] = inflow value of that stage
-  TileRegs<NP, EPL> pf;
-  tile_issue<NP, EPL, EDGE>(uin, e0, nd, pf);
-  tile_commit<NP, EPL>(pf, lds);
+  TileRegs<NP, W> pf;
+  tile_issue<NP, W, EDGE>(uin, e0, nd, pf);
+  tile_commit<NP, W>(pf, lds);
   if constexpr (EDGE) {
     // Lane-indexed read straight from the kernel-argument segment (k_step's args follow
     // its 4 pointer arguments): read as a uniform struct member, the compiler hoists these
     // 2*MS*NS SGPRs over the whole kernel and pushes the interior path into SGPR spills.
     using SArgs = StepArgs<NP, NS, MS>;
     const double* ka = reinterpret_cast<const double*>(
-        static_cast<const char*>(__builtin_amdgcn_kernarg_segment_ptr()) + 4 * sizeof(void*) +
+        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 4 * sizeof(void*) +
         offsetof(SArgs, uin));
     if (lane < MS * NS) lds[CB + lane] = ka[lane];
   }
@@ -404,7 +404,7 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
   double sc[EPL];
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
-    const int el = m * kBlock + lane;
+    const int el = m * LB + lane;
     to_eo<NP>(lds + pf.off + el * NP, ev[m], od[m]);
     E[m] = elem_info<H, T, EDGE>(e0, el, args.ktot, args.K);
     sc[m] = args.sc;
@@ -423,7 +423,7 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
       double pe[EPL][NE], po[EPL][NO];
 #pragma unroll
       for (int m = 0; m < EPL; ++m) {
-        const int el = m * kBlock + lane;
+        const int el = m * LB + lane;
         u0[m] = ev[m][0] + od[m][0];
         uN[m] = ev[m][0] - od[m][0];
         lds[fL + el + 1] = u0[m];
@@ -456,7 +456,7 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
       __syncthreads();
 #pragma unroll
       for (int m = 0; m < EPL; ++m) {
-        const int el = m * kBlock + lane;
+        const int el = m * LB + lane;
         // faceR[el] is element el-1's right node, faceL[el+2] element el+1's left node; the
         // pad entries are only read by the outermost halo elements, whose results are dropped.
         // Interior tiles: neighbours' faces.  Edge tiles: the first element of a
@@ -490,34 +490,34 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
     }
     if (snap != nullptr || st == MS - 1) {
       __syncthreads();  // the last stage's face reads are done before the image is rewritten
-      stage_out<NP, EPL, H>(lds, ev, od, false);
+      stage_out<NP, W, H>(lds, ev, od, false);
       __syncthreads();
       if constexpr (EDGE) {
-        if (snap != nullptr) store_run(snap + st * args.stride, o0, count, lds);
-        if (st == MS - 1 && last != nullptr) store_run(last, o0, count, lds);
+        if (snap != nullptr) store_run<LB>(snap + st * args.stride, o0, count, lds);
+        if (st == MS - 1 && last != nullptr) store_run<LB>(last, o0, count, lds);
       } else {
-        if (snap != nullptr) store_full<TE * NP>(snap + st * args.stride, o0, lds);
-        if (st == MS - 1 && last != nullptr) store_full<TE * NP>(last, o0, lds);
+        if (snap != nullptr) store_full<TE * NP, LB>(snap + st * args.stride, o0, lds);
+        if (st == MS - 1 && last != nullptr) store_full<TE * NP, LB>(last, o0, lds);
       }
       if (st < MS - 1) __syncthreads();  // the next stage's faces alias the image
     }
   }
 }
 
-template <int NP, int NS, bool UNI, int EPL, int MS>
-__global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
-                                                 double* __restrict__ snap,
-                                                 double* __restrict__ last,
-                                                 const double* __restrict__ scale,
-                                                 StepArgs<NP, NS, MS> args) {
-  using G = TileGeo<NP, EPL>;
+template <int NP, int NS, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_step(const double* __restrict__ uin,
+                                                     double* __restrict__ snap,
+                                                     double* __restrict__ last,
+                                                     const double* __restrict__ scale,
+                                                     StepArgs<NP, NS, MS> args) {
+  using G = TileGeo<NP, W>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * NS];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
   const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
   if (edge_tile(e0, G::T, args.ktot, args.K))
-    step_tile<NP, NS, UNI, EPL, MS, true>(lds, tile, uin, snap, last, scale, args);
+    step_tile<NP, NS, UNI, W, MS, true>(lds, tile, uin, snap, last, scale, args);
   else
-    step_tile<NP, NS, UNI, EPL, MS, false>(lds, tile, uin, snap, last, scale, args);
+    step_tile<NP, NS, UNI, W, MS, false>(lds, tile, uin, snap, last, scale, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kBlock) void k_step(const double* __restrict__ uin,
 // Indicator: eta += dt * sum_i w_i * s*(L0_i du0 + L1_i du1), with L0.w = le.we + lo.wo and
 // L1.w = -le.we + lo.wo.  The next snapshot tile is prefetched during each step's stages.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int EPL, int MS, bool EDGE>
+template <int NP, int NS, bool UNI, int W, int MS, bool EDGE>
 __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
                                          const double* __restrict__ win,
                                          double* __restrict__ wout,
@@ -538,8 +538,8 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
                                          double* __restrict__ eta,
                                          const double* __restrict__ scale,
                                          const AdjArgs<NP, MS>& args) {
-  using G = TileGeo<NP, EPL>;
-  constexpr int T = G::T;
+  using G = TileGeo<NP, W>;
+  constexpr int T = G::T, LB = G::LB, EPL = 1;
   constexpr int H = MS * NS;
   constexpr int TE = T - 2 * H;
   static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
@@ -549,14 +549,14 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
   const int64_t nd = args.ktot * NP;
 
   constexpr int CB = G::kLds;  // lds[CB + st] = inflow value at t_{n+st+1}; lds[CB + MS] = 0
-  TileRegs<NP, EPL> pw, pu;
-  tile_issue<NP, EPL, EDGE>(win, e0, nd, pw);
-  tile_issue<NP, EPL, EDGE>(snap + (MS - 1) * args.stride, e0, nd, pu);
-  tile_commit<NP, EPL>(pw, lds);
+  TileRegs<NP, W> pw, pu;
+  tile_issue<NP, W, EDGE>(win, e0, nd, pw);
+  tile_issue<NP, W, EDGE>(snap + (MS - 1) * args.stride, e0, nd, pu);
+  tile_commit<NP, W>(pw, lds);
   if constexpr (EDGE) {
     using AArgs = AdjArgs<NP, MS>;
     const double* ka = reinterpret_cast<const double*>(  // see step_tile; 5 pointer args
-        static_cast<const char*>(__builtin_amdgcn_kernarg_segment_ptr()) + 5 * sizeof(void*) +
+        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 5 * sizeof(void*) +
         offsetof(AArgs, uin_res));
     if (lane < MS) lds[CB + lane] = ka[lane];
     if (lane == MS) lds[CB + MS] = 0.0;
@@ -565,7 +565,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
   double we[EPL][NE], wo[EPL][NO];
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
-    const double* w = lds + pw.off + (m * kBlock + lane) * NP;
+    const double* w = lds + pw.off + (m * LB + lane) * NP;
 #pragma unroll
     for (int k = 0; k < NO; ++k) {
       we[m][k] = w[k] + w[N - k];
@@ -579,7 +579,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
   double eacc[EPL];
 #pragma unroll
   for (int m = 0; m < EPL; ++m) {
-    E[m] = elem_info<H, T, EDGE>(e0, m * kBlock + lane, args.ktot, args.K);
+    E[m] = elem_info<H, T, EDGE>(e0, m * LB + lane, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
     eacc[m] = 0.0;
@@ -588,13 +588,13 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 #pragma unroll
   for (int st = MS - 1; st >= 0; --st) {
     __syncthreads();  // previous reads of the image (w tile or the last stage's faces) done
-    tile_commit<NP, EPL>(pu, lds);
+    tile_commit<NP, W>(pu, lds);
     const int off = pu.off;
     __syncthreads();
-    if (st > 0) tile_issue<NP, EPL, EDGE>(snap + (st - 1) * args.stride, e0, nd, pu);
+    if (st > 0) tile_issue<NP, W, EDGE>(snap + (st - 1) * args.stride, e0, nd, pu);
 #pragma unroll
     for (int m = 0; m < EPL; ++m) {
-      const int el = m * kBlock + lane;
+      const int el = m * LB + lane;
       const double* us = lds + off + el * NP;
       if (args.src[st] != 0.0) {  // functional source (dual coordinates)
 #pragma unroll
@@ -646,7 +646,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
       double g0[EPL], g1[EPL];
 #pragma unroll
       for (int m = 0; m < EPL; ++m) {
-        const int el = m * kBlock + lane;
+        const int el = m * LB + lane;
         double gd = 0.0, gs = 0.0;
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
@@ -695,7 +695,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
       __syncthreads();
 #pragma unroll
       for (int m = 0; m < EPL; ++m) {
-        const int el = m * kBlock + lane;
+        const int el = m * LB + lane;
         // du0 = u_0 - (left neighbour's u_N); du1 = u_N - (right neighbour's u_0), with
         // u_0 = e_0 + o_0 and u_N = e_0 - o_0.
         // g1 of element k-1 and g0 of element k+1 (edge tiles: zero across trajectory ends)
@@ -711,32 +711,32 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
   for (int m = 0; m < EPL; ++m)
     if (args.has_eta && E[m].valid) eta[E[m].e] += eacc[m];
   __syncthreads();  // the last stage's face reads are done before the image is rewritten
-  stage_out<NP, EPL, H>(lds, we, wo, true);
+  stage_out<NP, W, H>(lds, we, wo, true);
   __syncthreads();
   const int64_t o0 = tile * TE * NP;
   if constexpr (EDGE) {
     const int64_t rem = nd - o0;
-    store_run(wout, o0, rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP, lds);
+    store_run<LB>(wout, o0, rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP, lds);
   } else {
-    store_full<TE * NP>(wout, o0, lds);
+    store_full<TE * NP, LB>(wout, o0, lds);
   }
 }
 
-template <int NP, int NS, bool UNI, int EPL, int MS>
-__global__ __launch_bounds__(kBlock) void k_adj(const double* __restrict__ win,
-                                                double* __restrict__ wout,
-                                                const double* __restrict__ snap,
-                                                double* __restrict__ eta,
-                                                const double* __restrict__ scale,
-                                                AdjArgs<NP, MS> args) {
-  using G = TileGeo<NP, EPL>;
+template <int NP, int NS, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_adj(const double* __restrict__ win,
+                                                    double* __restrict__ wout,
+                                                    const double* __restrict__ snap,
+                                                    double* __restrict__ eta,
+                                                    const double* __restrict__ scale,
+                                                    AdjArgs<NP, MS> args) {
+  using G = TileGeo<NP, W>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS + 1];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
   const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
   if (edge_tile(e0, G::T, args.ktot, args.K))
-    adj_tile<NP, NS, UNI, EPL, MS, true>(lds, tile, win, wout, snap, eta, scale, args);
+    adj_tile<NP, NS, UNI, W, MS, true>(lds, tile, win, wout, snap, eta, scale, args);
   else
-    adj_tile<NP, NS, UNI, EPL, MS, false>(lds, tile, win, wout, snap, eta, scale, args);
+    adj_tile<NP, NS, UNI, W, MS, false>(lds, tile, win, wout, snap, eta, scale, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -1008,8 +1008,8 @@ struct dg_plan {
   double* d_scratch2 = nullptr;
   double* d_pv = nullptr;
   int64_t* d_pi = nullptr;
-  // tuning (dg_plan_tune): elements per lane of the step kernels (tile = 256*epl elements)
-  int epl = 1;
+  // tuning (dg_plan_tune): tile width of the step kernels (tile = 256*tile_width elements)
+  int tile_width = 1;
   int msteps = 4;  // time steps fused per launch (1, 2 or 4)
   int xcd_order = 1;  // XCD-aware tile order
 };
@@ -1108,7 +1108,7 @@ template <int NP> LimArgs<NP> make_lim(const dg_plan* p) {
 
 inline unsigned grid_for(int64_t n, int64_t per) { return unsigned((n + per - 1) / per); }
 
-template <int NP, int NS, int EPL, int MS>
+template <int NP, int NS, int W, int MS>
 int launch_step_e(const dg_plan* p, const double* in, double* snap, double* last,
                   const double* times, double dt, hipStream_t st) {
   StepArgs<NP, NS, MS> a;
@@ -1120,19 +1120,19 @@ int launch_step_e(const dg_plan* p, const double* in, double* snap, double* last
   a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
   a.xcd = p->xcd_order;
-  constexpr int TE = kBlock * EPL - 2 * MS * NS;
+  constexpr int TE = kBlock * W - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_step<NP, NS, true, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, in,
+    hipLaunchKernelGGL((k_step<NP, NS, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
                        snap, last, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_step<NP, NS, false, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, in,
+    hipLaunchKernelGGL((k_step<NP, NS, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
                        snap, last, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-template <int NP, int NS, int EPL, int MS>
+template <int NP, int NS, int W, int MS>
 int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double* snap,
                  double* eta, const double* t_next, const double* src, double dt,
                  hipStream_t st) {
@@ -1148,34 +1148,32 @@ int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr;
   a.xcd = p->xcd_order;
-  constexpr int TE = kBlock * EPL - 2 * MS * NS;
+  constexpr int TE = kBlock * W - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_adj<NP, NS, true, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, win,
+    hipLaunchKernelGGL((k_adj<NP, NS, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
                        wout, snap, eta, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_adj<NP, NS, false, EPL, MS>), dim3(grid), dim3(kBlock), 0, st, win,
+    hipLaunchKernelGGL((k_adj<NP, NS, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
                        wout, snap, eta, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-// Instantiated shapes: (elements per lane, steps per launch) in {(1,1), (2,1), (1,2), (1,4)},
-// plus (2,2), (2,4) for Np <= 6;
-// 4 steps per launch only for Np <= 8 (at Np = 9 hipcc/ROCm 7.2 fails instruction
-// selection for that shape; chunk() never asks for it there).
+// Instantiated shapes: tile width W in {1, 2} (256 or 512 elements per tile) x steps per
+// launch in {1, 2, 4}; 4 steps per launch only for Np <= 8 (at Np = 9 hipcc/ROCm 7.2 fails
+// instruction selection for that shape; chunk() never asks for it there).
 template <int NP, int NS>
 int launch_step_t(const dg_plan* p, int ms, const double* in, double* snap, double* last,
                   const double* times, double dt, hipStream_t st) {
+  const bool w2 = p->tile_width == 2;
   if constexpr (NP <= 8) {
-    if (ms == 4 && p->epl == 2 && NP <= 6)
-      return launch_step_e<NP, NS, 2, 4>(p, in, snap, last, times, dt, st);
+    if (ms == 4 && w2) return launch_step_e<NP, NS, 2, 4>(p, in, snap, last, times, dt, st);
     if (ms == 4) return launch_step_e<NP, NS, 1, 4>(p, in, snap, last, times, dt, st);
   }
-  if (ms == 2 && p->epl == 2 && NP <= 6)
-    return launch_step_e<NP, NS, 2, 2>(p, in, snap, last, times, dt, st);
+  if (ms == 2 && w2) return launch_step_e<NP, NS, 2, 2>(p, in, snap, last, times, dt, st);
   if (ms == 2) return launch_step_e<NP, NS, 1, 2>(p, in, snap, last, times, dt, st);
-  if (p->epl == 2) return launch_step_e<NP, NS, 2, 1>(p, in, snap, last, times, dt, st);
+  if (w2) return launch_step_e<NP, NS, 2, 1>(p, in, snap, last, times, dt, st);
   return launch_step_e<NP, NS, 1, 1>(p, in, snap, last, times, dt, st);
 }
 
@@ -1183,16 +1181,16 @@ template <int NP, int NS>
 int launch_adj_t(const dg_plan* p, int ms, const double* win, double* wout, const double* snap,
                  double* eta, const double* t_next, const double* src, double dt,
                  hipStream_t st) {
+  const bool w2 = p->tile_width == 2;
   if constexpr (NP <= 8) {
-    if (ms == 4 && p->epl == 2 && NP <= 6)
+    if (ms == 4 && w2)
       return launch_adj_e<NP, NS, 2, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
     if (ms == 4) return launch_adj_e<NP, NS, 1, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
   }
-  if (ms == 2 && p->epl == 2 && NP <= 6)
+  if (ms == 2 && w2)
     return launch_adj_e<NP, NS, 2, 2>(p, win, wout, snap, eta, t_next, src, dt, st);
   if (ms == 2) return launch_adj_e<NP, NS, 1, 2>(p, win, wout, snap, eta, t_next, src, dt, st);
-  if (p->epl == 2)
-    return launch_adj_e<NP, NS, 2, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
+  if (w2) return launch_adj_e<NP, NS, 2, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
   return launch_adj_e<NP, NS, 1, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
 }
 
@@ -1311,9 +1309,9 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   p->s_uniform = 2.0 / hmean;
 
   {
-    if (const char* v = std::getenv("DG_ELEMS_PER_LANE")) {
+    if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);
-      if (k == 1 || k == 2) p->epl = k;
+      if (k == 1 || k == 2) p->tile_width = k;
     }
     if (const char* v = std::getenv("DG_STEPS_PER_LAUNCH")) {
       const int k = std::atoi(v);
@@ -1361,7 +1359,7 @@ int dg_plan_query(const dg_plan* p, int64_t out[8]) {
   out[3] = p->batch;
   out[4] = p->uniform ? 1 : 0;
   out[5] = p->nstages;
-  out[6] = p->epl;
+  out[6] = p->tile_width;
   out[7] = (p->NP > 8 && p->msteps > 2) ? 2 : p->msteps;
   return DG_OK;
 }
@@ -1369,9 +1367,9 @@ int dg_plan_query(const dg_plan* p, int64_t out[8]) {
 int dg_plan_tune(dg_plan* p, int key, int64_t value) {
   if (!p) return fail(DG_ERR_ARG, "null plan");
   switch (key) {
-    case DG_TUNE_ELEMS_PER_LANE:
-      if (value != 1 && value != 2) return fail(DG_ERR_ARG, "elements per lane must be 1 or 2");
-      p->epl = int(value);
+    case DG_TUNE_TILE_WIDTH:
+      if (value != 1 && value != 2) return fail(DG_ERR_ARG, "tile width must be 1 or 2");
+      p->tile_width = int(value);
       return DG_OK;
     case DG_TUNE_XCD_ORDER:
       p->xcd_order = value ? 1 : 0;

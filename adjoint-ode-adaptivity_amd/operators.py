@@ -81,7 +81,7 @@ class DGAdvection1D:
     _lib.check(self._lib.dg_plan_query(self._plan, q), "dg_plan_query")
     self.uniform = bool(q[4])
     self.stages = int(q[5])
-    self.elems_per_lane = int(q[6])
+    self.tile_width = int(q[6])
     self.steps_per_launch = int(q[7])
 
   # --- lifetime ---
@@ -102,18 +102,18 @@ class DGAdvection1D:
   def __exit__(self, *exc):
     self.close()
 
-  def tune(self, elems_per_lane=None, steps_per_launch=None, xcd_order=None):
-    """Shape of the fused step kernels: each lane holds ``elems_per_lane`` elements (1 or
-    2), ``steps_per_launch`` (1, 2 or 4) time steps are fused per launch, and
-    ``xcd_order`` gives each XCD a contiguous range of tiles.  Elements per lane and the
-    tile order do not change the arithmetic; steps per launch changes it at rounding
-    level (the state stays in even/odd coordinates between fused steps)."""
+  def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None):
+    """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
+    element per lane), ``steps_per_launch`` (1, 2 or 4) time steps fused per launch, and
+    ``xcd_order`` gives each XCD a contiguous range of tiles.  Tile width and order do not
+    change the arithmetic; steps per launch changes it at rounding level (the state stays
+    in even/odd coordinates between fused steps)."""
     if xcd_order is not None:
       _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_XCD_ORDER, int(xcd_order)),
                  "dg_plan_tune")
-    if elems_per_lane is not None:
-      _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_ELEMS_PER_LANE,
-                                        int(elems_per_lane)), "dg_plan_tune")
+    if tile_width is not None:
+      _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_TILE_WIDTH,
+                                        int(tile_width)), "dg_plan_tune")
     if steps_per_launch is not None:
       _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_STEPS_PER_LAUNCH,
                                         int(steps_per_launch)), "dg_plan_tune")

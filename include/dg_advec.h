@@ -73,18 +73,19 @@ int dg_plan_create(int N, int64_t K, int64_t batch,
 int dg_plan_destroy(dg_plan* plan);
 
 /* Query plan sizes: out[0]=N, out[1]=Np, out[2]=K, out[3]=batch, out[4]=uniform mesh (0/1),
- * out[5]=time stages per step, out[6]=elements per lane, out[7]=time steps per launch. */
+ * out[5]=time stages per step, out[6]=tile width, out[7]=time steps per launch. */
 int dg_plan_query(const dg_plan* plan, int64_t out[8]);
 
-/* Tuning knobs of the fused step kernels (results are bit-identical for every setting).
- *   DG_TUNE_ELEMS_PER_LANE    elements held per lane: 1 or 2 (tile = 256*value elements;
- *                             2 with 2 or 4 steps per launch needs Np <= 6)
+/* Tuning knobs of the fused step kernels.  Tile width and tile order leave the arithmetic
+ * bit-identical; steps per launch changes it at rounding level only.
+ *   DG_TUNE_TILE_WIDTH        1 or 2: workgroups of 256*value lanes, one element per lane,
+ *                             own tiles of 256*value elements (2: half the halo overhead)
  *   DG_TUNE_STEPS_PER_LAUNCH  time steps fused per launch: 1, 2 or 4 (temporal blocking:
  *                             each launch reads its input state once and writes every
  *                             intermediate snapshot; halo = steps*stages elements per side)
  *   DG_TUNE_XCD_ORDER         0/1: give each XCD a contiguous range of tiles (speed only)
- * Environment overrides at plan creation: DG_ELEMS_PER_LANE, DG_STEPS_PER_LAUNCH. */
-enum { DG_TUNE_ELEMS_PER_LANE = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3 };
+ * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH. */
+enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* rhs = AdvecRHS1D(u, t, a)   — utils/AdvecRHS1D.m:1-20 (inline copy One_code.mlx:124-134).

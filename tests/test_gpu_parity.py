@@ -337,8 +337,8 @@ def test_kernel_variants_bit_identical(pkg, gpu, N, K):
   outs = []
   nsteps = 7  # exercises the greedy 4 + 2 + 1 chunking
   shapes = ((1, 1, 1), (2, 1, 0), (1, 2, 1), (1, 4, 1), (2, 4, 0), (1, 4, 0), (2, 2, 1))
-  for epl, ms, xcd in shapes:
-    op = make_op(pkg, mesh).tune(elems_per_lane=epl, steps_per_launch=ms, xcd_order=xcd)
+  for width, ms, xcd in shapes:
+    op = make_op(pkg, mesh).tune(tile_width=width, steps_per_launch=ms, xcd_order=xcd)
     snaps = op.new_field(nsteps + 1)
     op.forward(u0.clone(), 0.0, dt, nsteps, snaps)
     w = snaps[nsteps].clone()
