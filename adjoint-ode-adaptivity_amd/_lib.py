@@ -16,6 +16,8 @@ DG_OK, DG_ERR_ARG, DG_ERR_HIP, DG_ERR_NOMEM = 0, -1, -2, -3
 DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T = 0, 1
 DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
 DG_TUNE_TILE_WIDTH, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
+DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
+DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE = 0, 1
 
 _c_dbl_p = ctypes.POINTER(ctypes.c_double)
 _vp = ctypes.c_void_p
@@ -31,6 +33,10 @@ SIGNATURES = {
     "dg_plan_destroy": (_i32, [_vp]),
     "dg_plan_query": (_i32, [_vp, ctypes.POINTER(_i64)]),
     "dg_plan_tune": (_i32, [_vp, _i32, _i64]),
+    "dg_plan_set_physics": (_i32, [_vp, _i32, _i32]),
+    "dg_plan_reserve": (_i32, [_vp, _i64]),
+    "dg_plan_refine": (_i32, [_vp, _vp, _vp, _vp]),
+    "dg_plan_get_mesh": (_i32, [_vp, _c_dbl_p]),
     "dg_advec_rhs": (_i32, [_vp, _vp, _vp, ctypes.c_double, _vp]),
     "dg_lserk4_fwd": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp]),
     "dg_lserk4_adj": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32,

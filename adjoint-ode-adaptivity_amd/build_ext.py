@@ -1,6 +1,8 @@
-"""Build the HIP extension in-tree: csrc/dg_advec.hip -> lib/libdgadv.so (gfx950).
+"""Build the HIP extension in-tree: csrc/*.hip -> lib/libdgadv.so (gfx950).
 
-hipcc cross-compiles without a GPU; the .so travels to the GPU box with the tree.
+Each translation unit is compiled to an object in parallel (they are template-heavy), then
+linked into one shared library.  hipcc cross-compiles without a GPU; the .so travels to the
+GPU box with the tree.
 """
 import os
 import shutil
@@ -8,7 +10,8 @@ import subprocess
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(_HERE, "csrc", "dg_advec.hip")
+SRCS = [os.path.join(_HERE, "csrc", f) for f in ("dg_advec.hip", "dg_burgers.hip")]
+COMMON = os.path.join(_HERE, "csrc", "dg_common.h")
 INCLUDE = os.path.normpath(os.path.join(_HERE, "..", "include"))
 OUT = os.path.join(_HERE, "lib", "libdgadv.so")
 ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
@@ -22,21 +25,33 @@ def hipcc():
 
 
 def build(force=False, verbose=True, extra_flags=()):
-  deps = [SRC, os.path.join(INCLUDE, "dg_advec.h")]
+  deps = SRCS + [COMMON, os.path.join(INCLUDE, "dg_advec.h")]
   if (not force and os.path.exists(OUT)
       and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps)):
     if verbose:
       print(f"[build_ext] up to date: {OUT}")
     return OUT
   os.makedirs(os.path.dirname(OUT), exist_ok=True)
+  objdir = os.path.join(os.path.dirname(OUT), "obj")
+  os.makedirs(objdir, exist_ok=True)
+  flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-I", INCLUDE, *extra_flags]
+  procs, objs = [], []
+  for src in SRCS:
+    obj = os.path.join(objdir, os.path.basename(src) + ".o")
+    cmd = [hipcc(), *flags, "-c", "-o", obj, src]
+    if verbose:
+      print("[build_ext]", " ".join(cmd))
+    procs.append((subprocess.Popen(cmd), src))
+    objs.append(obj)
+  failed = [src for p, src in procs if p.wait() != 0]
+  if failed:
+    raise RuntimeError(f"hipcc failed on {failed}; {OUT} was NOT updated")
   tmp = OUT + ".tmp"
-  cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-         "-I", INCLUDE, *extra_flags, "-o", tmp, SRC]
+  cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
   if verbose:
     print("[build_ext]", " ".join(cmd))
-  r = subprocess.run(cmd)
-  if r.returncode != 0:
-    raise RuntimeError(f"hipcc failed ({r.returncode}); {OUT} was NOT updated")
+  if subprocess.run(cmd).returncode != 0:
+    raise RuntimeError(f"link failed; {OUT} was NOT updated")
   os.replace(tmp, OUT)
   return OUT
 

@@ -1,0 +1,823 @@
+// dg_burgers.hip — the nonlinear-flux / per-stage-limiter path (BASELINE config 3,
+// SURVEY §8(f)1): SlopeLimitN (utils/SlopeLimitN.m:1-33, SlopeLimitLin.m, minmod.m) applied
+// after every LSERK4 stage update (utils/One_code.mlx:135-136) and, optionally, the
+// build-defined Burgers-type flux f(u) = a*u^2/2 with AdvecRHS1D's central-flux structure
+// (utils/AdvecRHS1D.m:9-19 with a*u -> a*f(u); CPU statement: oracle/burgers.py).
+//
+//   k_step_nl<NP,BURG,LIM,UNI,MS>  MS fused limited steps per launch.  Same tile scheme as
+//       k_step (one element per lane, 256-element tiles, state in VGPRs, faces exchanged
+//       through LDS); the limiter adds one cell-average exchange per stage, so the
+//       dependency cone is 2 elements per stage (1 without the limiter).
+//   k_adj_nl<NP,BURG,LIM,UNI>  one reverse step per launch: it recomputes the step's 5
+//       stages from u^n in registers (keeping each stage input and the limiter's decision:
+//       troubled or not, and which minmod argument was active), then runs the exact
+//       transpose of the stages' tangent — the limiter with its decisions frozen, the flux
+//       Jacobian diag(f'(u)) = diag(a*u) at the recomputed stage inputs — and accumulates
+//       the dual-weighted jump residual of u^{n+1} into eta.
+//   k_rhs_nl<NP>  the Burgers RHS for parity tests.
+//
+// Limiter arithmetic.  On a troubled cell SlopeLimitN replaces u by
+//   y_i = v + (x_i - x0) m,   m = minmod(ux(1), (v+ - v)/h, (v - v-)/h)   (SlopeLimitLin.m:10-18)
+// and x_i - x0 = h r_i / 2 for the LGL nodes, so with hm = h*m
+//   y_i = v + (r_i / 2) hm,   hm = minmod(2 (Dr V)(1,1:2) uh(1:2), v+ - v, v - v-)
+// (h > 0 scales all three arguments alike): no mesh coordinates are needed, on any mesh.
+#include "dg_common.h"
+
+namespace {
+using namespace dgk;
+
+// Limiter constants in even/odd coordinates (host: make_lim_eo).
+template <int NP> struct LimEO {
+  static constexpr int NE = (NP + 1) / 2, NO = NP / 2;
+  double a0e[NE], a0o[NO];  // uh(1) = sum_j invV(1,j) v_j = a0e.e + a0o.o   (SlopeLimitN.m:9)
+  double a1e[NE], a1o[NO];  // uh(2) = sum_j invV(2,j) v_j                    (SlopeLimitN.m:28)
+  double V00;               // cell average = V(1,1) uh(1)
+  double dv0, dv1;          // (Dr*ul)(1) = dv0 uh(1) + dv1 uh(2)             (SlopeLimitLin.m:16)
+  double rce[NE], rco[NO];  // r_i / 2 in even/odd form: y = v + r/2 hm
+};
+
+// minmod (utils/minmod.m:6-12) of three values and which one it returned: 1..3, or 0 when
+// the signs differ (result 0).  Ties go to the first argument (min keeps the first).
+__device__ __forceinline__ double minmod_br(double a, double b, double c, int& br) {
+  const bool pos = a > 0.0 && b > 0.0 && c > 0.0;
+  const bool neg = a < 0.0 && b < 0.0 && c < 0.0;
+  br = 0;
+  if (!pos && !neg) return 0.0;
+  double m = fabs(a);
+  br = 1;
+  if (fabs(b) < m) {
+    m = fabs(b);
+    br = 2;
+  }
+  if (fabs(c) < m) {
+    m = fabs(c);
+    br = 3;
+  }
+  return pos ? m : -m;
+}
+
+// The troubled-cell test of SlopeLimitN.m:21-23.
+__device__ __forceinline__ bool troubled(double v, double vm, double vp, double u0, double uN) {
+  int br;
+  const double ve1 = v - minmod_br(v - u0, v - vm, vp - v, br);
+  const double ve2 = v + minmod_br(uN - v, v - vm, vp - v, br);
+  return fabs(ve1 - u0) > 1.0e-8 || fabs(ve2 - uN) > 1.0e-8;
+}
+
+// Flux values divided by a, in even/odd coordinates: f = u (linear) or u^2/2 (Burgers):
+//   fe_k = (f_k + f_{N-k})/2 = (e^2 + o^2)/2,  fo_k = (f_k - f_{N-k})/2 = e o.
+template <int NP, bool BURG>
+__device__ __forceinline__ void flux_eo(const double* ev, const double* od, double* fe,
+                                        double* fo) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    fe[k] = BURG ? 0.5 * fma(ev[k], ev[k], od[k] * od[k]) : ev[k];
+    fo[k] = BURG ? ev[k] * od[k] : od[k];
+  }
+  if constexpr (NE > NO) fe[NO] = BURG ? 0.5 * ev[NO] * ev[NO] : ev[NO];
+}
+
+// Exchange arrays in LDS (doubles, each padded by one slot on the left): two
+// double-buffered face pairs [0, 4(T+2)), cell averages [4(T+2), 5(T+2)), the adjoint's
+// limiter contributions to the left / right neighbour [5(T+2), 7(T+2)).
+template <int NP> struct NLGeo {
+  static constexpr int T = kBlock;
+  static constexpr int FA = 4 * (T + 2), CL = 5 * (T + 2), CR = 6 * (T + 2);
+  static constexpr int kEx = 7 * (T + 2);
+  static constexpr int kTileD = T * NP + 2;
+  static constexpr int kLds = kTileD > kEx ? kTileD : kEx;  // boundary constants follow
+};
+
+// One LSERK4 stage s of the lane's element:  r = A_s r + dt RHS(u);  v = u + B_s r;
+// u = SlopeLimitN(v) if LIM.  Returns the limiter's decision: 0 if the cell is not
+// troubled, else 4 | (the active minmod argument, 0..3).  iin: LDS slot of the stage's
+// inflow flux f(uin).  Barriers: one (faces), two with the limiter (cell averages).
+template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE>
+__device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s, int iin,
+                                        const Elem& E, double sc, const EOArgs<NP>& op,
+                                        const LimEO<NP>& lc, double* ev, double* od,
+                                        double* re, double* ro) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, T = kBlock;
+  constexpr int FA = NLGeo<NP>::FA;
+  const int fL = (s & 1) * 2 * (T + 2), fR = fL + (T + 2);
+  double fe[NE], fo[NO];
+  flux_eo<NP, BURG>(ev, od, fe, fo);
+  const double f0 = fe[0] + fo[0], fN = fe[0] - fo[0];
+  lds[fL + el + 1] = f0;
+  lds[fR + el + 1] = fN;
+  __builtin_amdgcn_sched_barrier(0);
+  double pe[NE], po[NO];  // volume term (+ the carry A_s r on uniform meshes)
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    double t = (UNI && s > 0) ? RK<5>::A(s) * re[k] : op.Qeo[k * NO] * fo[0];
+#pragma unroll
+    for (int j = (UNI && s > 0) ? 0 : 1; j < NO; ++j) t = fma(op.Qeo[k * NO + j], fo[j], t);
+    pe[k] = t;
+  }
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    double t = (UNI && s > 0) ? RK<5>::A(s) * ro[k] : op.Qoe[k * NE] * fe[0];
+#pragma unroll
+    for (int j = (UNI && s > 0) ? 0 : 1; j < NE; ++j) t = fma(op.Qoe[k * NE + j], fe[j], t);
+    po[k] = t;
+  }
+#pragma unroll
+  for (int k = 0; k < NE; ++k) pin(pe[k]);
+#pragma unroll
+  for (int k = 0; k < NO; ++k) pin(po[k]);
+  __syncthreads();
+  // Neighbour fluxes: left element's right face, right element's left face; a
+  // trajectory's first element reads the inflow flux, its last one its own face (du1 = 0).
+  const int iL = EDGE && E.first ? iin : fR + el;
+  const int iR = EDGE && E.last ? fR + el + 1 : fL + el + 2;
+  const double du0 = f0 - lds[iL];
+  const double du1 = fN - lds[iR];
+  const double dlt = du0 - du1, sig = du0 + du1;
+#pragma unroll
+  for (int k = 0; k < NE; ++k) {
+    if constexpr (UNI) {
+      re[k] = fma(op.le[k], dlt, pe[k]);
+    } else {
+      const double a = sc * fma(op.le[k], dlt, pe[k]);
+      re[k] = (s == 0) ? a : fma(RK<5>::A(s), re[k], a);
+    }
+    ev[k] = fma(RK<5>::B(s), re[k], ev[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    if constexpr (UNI) {
+      ro[k] = fma(op.lo[k], sig, po[k]);
+    } else {
+      const double a = sc * fma(op.lo[k], sig, po[k]);
+      ro[k] = (s == 0) ? a : fma(RK<5>::A(s), ro[k], a);
+    }
+    od[k] = fma(RK<5>::B(s), ro[k], od[k]);
+  }
+  if constexpr (!LIM) {
+    return 0;
+  } else {
+    double uh0 = lc.a0e[0] * ev[0];
+#pragma unroll
+    for (int k = 1; k < NE; ++k) uh0 = fma(lc.a0e[k], ev[k], uh0);
+#pragma unroll
+    for (int k = 0; k < NO; ++k) uh0 = fma(lc.a0o[k], od[k], uh0);
+    const double avg = lc.V00 * uh0;
+    lds[FA + el + 1] = avg;
+    __syncthreads();
+    // Neighbour averages, replicated at a trajectory's ends (SlopeLimitN.m:18).
+    const double am = lds[EDGE && E.first ? FA + el + 1 : FA + el];
+    const double ap = lds[EDGE && E.last ? FA + el + 1 : FA + el + 2];
+    if (!troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0])) return 0;
+    double uh1 = lc.a1e[0] * ev[0];
+#pragma unroll
+    for (int k = 1; k < NE; ++k) uh1 = fma(lc.a1e[k], ev[k], uh1);
+#pragma unroll
+    for (int k = 0; k < NO; ++k) uh1 = fma(lc.a1o[k], od[k], uh1);
+    int br;
+    const double hm = minmod_br(2.0 * fma(lc.dv0, uh0, lc.dv1 * uh1), ap - avg, avg - am, br);
+#pragma unroll
+    for (int k = 0; k < NE; ++k) ev[k] = fma(lc.rce[k], hm, avg);
+#pragma unroll
+    for (int k = 0; k < NO; ++k) od[k] = lc.rco[k] * hm;
+    return 4 | br;
+  }
+}
+
+// Interior elements [H, T-H) of the tile to LDS (element-major, nodal); dual = adjoint
+// coordinates (w_k = (we + wo)/2, w_{N-k} = (we - wo)/2).
+template <int NP, int H>
+__device__ __forceinline__ void put_interior(double* __restrict__ lds, const double* ev,
+                                             const double* od, bool dual) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1, T = kBlock;
+  const int el = threadIdx.x;
+  if (el >= H && el < T - H) {
+    double* o = lds + (el - H) * NP;
+    if (dual) {
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        o[k] = 0.5 * (ev[k] + od[k]);
+        o[N - k] = 0.5 * (ev[k] - od[k]);
+      }
+      if constexpr (NE > NO) o[NO] = ev[NO];
+    } else {
+      from_eo<NP>(ev, od, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward: MS limited steps per launch.
+// ---------------------------------------------------------------------------
+template <int NP, int MS> struct NLStepArgs {
+  EOArgs<NP> op;
+  LimEO<NP> lc;
+  double sc;           // dt (non-uniform meshes multiply by scale[k]; uniform: folded in op)
+  double fin[MS * 5];  // inflow flux f(uin) at each stage time
+  int64_t ktot;
+  int64_t stride;      // doubles between consecutive snapshots
+  int32_t K;
+  int32_t xcd;
+};
+
+template <bool LIM> constexpr int cone_per_stage() { return LIM ? 2 : 1; }
+
+template <int NP, bool BURG, bool LIM, bool UNI, int MS, bool EDGE>
+__device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t tile,
+                                             const double* __restrict__ uin,
+                                             double* __restrict__ snap, double* __restrict__ last,
+                                             const double* __restrict__ scale,
+                                             const NLStepArgs<NP, MS>& args) {
+  constexpr int T = kBlock, NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
+  constexpr int H = MS * 5 * cone_per_stage<LIM>();
+  constexpr int TE = T - 2 * H;
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int CB = NLGeo<NP>::kLds;  // lds[CB + st*5 + s] = inflow flux of that stage
+  const int lane = threadIdx.x;
+  const int64_t e0 = tile * TE - H;
+  const int64_t nd = args.ktot * NP;
+  const int64_t o0 = tile * TE * NP;
+  const int64_t rem = nd - o0;
+  const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
+
+  TileRegs<NP, 1> pf;
+  tile_issue<NP, 1, EDGE>(uin, e0, nd, pf);
+  tile_commit<NP, 1>(pf, lds);
+  if constexpr (EDGE) {
+    // Lane-indexed read of fin straight from the kernel-argument segment (the args follow
+    // the 4 pointer arguments of k_step_nl), as in k_step.
+    using SArgs = NLStepArgs<NP, MS>;
+    const double* ka = reinterpret_cast<const double*>(
+        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 4 * sizeof(void*) +
+        offsetof(SArgs, fin));
+    if (lane < MS * 5) lds[CB + lane] = ka[lane];
+  }
+  __syncthreads();
+  double ev[NE], od[NO];
+  to_eo<NP>(lds + pf.off + lane * NP, ev, od);
+  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  double sc = args.sc;
+  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
+  __syncthreads();  // the exchange arrays alias the staging image
+
+  double re[NE], ro[NO];
+#pragma unroll
+  for (int st = 0; st < MS; ++st) {
+#pragma unroll
+    for (int s = 0; s < 5; ++s)
+      nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, CB + st * 5 + s, E, sc, args.op, args.lc,
+                                         ev, od, re, ro);
+    if (snap != nullptr || st == MS - 1) {
+      __syncthreads();  // the last stage's exchange reads are done before the image is rewritten
+      put_interior<NP, H>(lds, ev, od, false);
+      __syncthreads();
+      if constexpr (EDGE) {
+        if (snap != nullptr) store_run<T>(snap + st * args.stride, o0, count, lds);
+        if (st == MS - 1 && last != nullptr) store_run<T>(last, o0, count, lds);
+      } else {
+        if (snap != nullptr) store_full<TE * NP, T>(snap + st * args.stride, o0, lds);
+        if (st == MS - 1 && last != nullptr) store_full<TE * NP, T>(last, o0, lds);
+      }
+      if (st < MS - 1) __syncthreads();  // the next stage's exchange arrays alias the image
+    }
+  }
+}
+
+template <int NP, bool BURG, bool LIM, bool UNI, int MS>
+__global__ __launch_bounds__(kBlock) void k_step_nl(const double* __restrict__ uin,
+                                                    double* __restrict__ snap,
+                                                    double* __restrict__ last,
+                                                    const double* __restrict__ scale,
+                                                    NLStepArgs<NP, MS> args) {
+  constexpr int T = kBlock, H = MS * 5 * cone_per_stage<LIM>();
+  __shared__ __attribute__((aligned(16))) double lds[NLGeo<NP>::kLds + MS * 5];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  const int64_t e0 = tile * (T - 2 * H) - H;
+  if (edge_tile(e0, T, args.ktot, args.K))
+    nl_step_tile<NP, BURG, LIM, UNI, MS, true>(lds, tile, uin, snap, last, scale, args);
+  else
+    nl_step_tile<NP, BURG, LIM, UNI, MS, false>(lds, tile, uin, snap, last, scale, args);
+}
+
+// ---------------------------------------------------------------------------
+// Adjoint: one reverse step per launch (w^{n+1} -> w^n), stages recomputed from u^n.
+// ---------------------------------------------------------------------------
+template <int NP> struct NLAdjArgs {
+  EOArgs<NP> op;
+  LimEO<NP> lc;
+  double sc;
+  double fin[6];   // inflow flux at the 5 stage times of step n, then at t_{n+1} (residual)
+  double src;      // functional source coefficient of node n+1
+  int64_t ktot;
+  int32_t K;
+  int32_t has_eta;
+  int32_t xcd;
+};
+
+template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE>
+__device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t tile,
+                                            const double* __restrict__ win,
+                                            double* __restrict__ wout,
+                                            const double* __restrict__ snap,
+                                            double* __restrict__ eta,
+                                            const double* __restrict__ scale,
+                                            const NLAdjArgs<NP>& args) {
+  constexpr int T = kBlock, NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  // forward recompute and reverse sweep each widen the cone by one stage-cone per stage
+  constexpr int H = 10 * cone_per_stage<LIM>();
+  constexpr int TE = T - 2 * H;
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int CB = NLGeo<NP>::kLds;  // lds[CB+s]: stage inflow flux; CB+5: residual's; CB+6: 0
+  constexpr int CL = NLGeo<NP>::CL, CR = NLGeo<NP>::CR;
+  const int lane = threadIdx.x;
+  const int64_t e0 = tile * TE - H;
+  const int64_t nd = args.ktot * NP;
+
+  TileRegs<NP, 1> pu, pw;
+  tile_issue<NP, 1, EDGE>(snap, e0, nd, pu);
+  tile_issue<NP, 1, EDGE>(win, e0, nd, pw);
+  tile_commit<NP, 1>(pu, lds);
+  if constexpr (EDGE) {
+    using AArgs = NLAdjArgs<NP>;  // the args follow the 5 pointer arguments of k_adj_nl
+    const double* ka = reinterpret_cast<const double*>(
+        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 5 * sizeof(void*) +
+        offsetof(AArgs, fin));
+    if (lane < 6) lds[CB + lane] = ka[lane];
+    if (lane == 6) lds[CB + 6] = 0.0;
+  }
+  __syncthreads();
+  double ev[NE], od[NO];
+  to_eo<NP>(lds + pu.off + lane * NP, ev, od);
+  __syncthreads();
+  tile_commit<NP, 1>(pw, lds);
+  __syncthreads();
+  double we[NE], wo[NO];  // the adjoint in dual even/odd coordinates
+  {
+    const double* w = lds + pw.off + lane * NP;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      we[k] = w[k] + w[N - k];
+      wo[k] = w[k] - w[N - k];
+    }
+    if constexpr (NE > NO) we[NO] = w[NO];
+  }
+  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  double sc = args.sc;
+  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
+  __syncthreads();  // the exchange arrays alias the staging image
+
+  // 1. Recompute the step's stages, keeping each stage's input and limiter decision.
+  double se[5][NE], so[5][NO];
+  int codes = 0;
+  {
+    double re[NE], ro[NO];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+#pragma unroll
+      for (int k = 0; k < NE; ++k) se[s][k] = ev[k];
+#pragma unroll
+      for (int k = 0; k < NO; ++k) so[s][k] = od[k];
+      const int c = nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, CB + s, E, sc, args.op,
+                                                       args.lc, ev, od, re, ro);
+      if constexpr (LIM) codes |= c << (3 * s);
+    }
+  }
+  // (ev, od) = u^{n+1}.  2. Functional source w^{n+1} += src u^{n+1} (dual coordinates).
+  if (args.src != 0.0) {
+    const double s2 = 2.0 * args.src;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      we[k] = fma(s2, ev[k], we[k]);
+      wo[k] = fma(s2, od[k], wo[k]);
+    }
+    if constexpr (NE > NO) we[NO] = fma(args.src, ev[NO], we[NO]);
+  }
+  // 3. Indicator: eta += dt sum_i w_i (LIFT Fscale du)_i at u^{n+1}, t_{n+1}.
+  double eacc = 0.0;
+  if (args.has_eta) {
+    double fe[NE], fo[NO];
+    flux_eo<NP, BURG>(ev, od, fe, fo);
+    const double f0 = fe[0] + fo[0], fN = fe[0] - fo[0];
+    constexpr int gL = 2 * (T + 2), gR = gL + (T + 2);  // face buffer 1 (stage 4 used 0)
+    lds[gL + lane + 1] = f0;
+    lds[gR + lane + 1] = fN;
+    __syncthreads();
+    const double du0 = f0 - lds[EDGE && E.first ? CB + 5 : gR + lane];
+    const double du1 = fN - lds[EDGE && E.last ? gR + lane + 1 : gL + lane + 2];
+    double pe = 0.0, po = 0.0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[k], pe);
+#pragma unroll
+    for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[k], po);
+    eacc = fma(du0 - du1, pe, (du0 + du1) * po);
+    if constexpr (!UNI) eacc *= sc;
+  }
+  __syncthreads();  // exchange reads of the last stage / the indicator are done
+
+  // 4. Reverse stages s = 4..0 (forward: r = A_s r + dt L f(u); v = u + B_s r; u = Lim(v)):
+  //      lv = Lim'(v)^T lu;  lr += B_s lv;  lu = lv + f'(u_s) (dt L^T lr);  lr = A_s lr.
+  double lre[NE], lro[NO];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) lre[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < NO; ++k) lro[k] = 0.0;
+#pragma unroll
+  for (int ss = 0; ss < 5; ++ss) {
+    const int s = 4 - ss;
+    if constexpr (LIM) {
+      // Transposed limiter.  Troubled cell: y = v_avg + (r/2) hm, hm one of
+      // {2 (Dr V)(1,:) uh(1:2), v+ - v, v - v-} (or 0): the cell's own nodal adjoint is
+      // replaced by the branch-1 gradient, and avg-adjoints go to this cell (cs) and to the
+      // left / right neighbour (cl / cr).  Every cell then adds the avg-adjoint it
+      // receives times d avg / d v.
+      const int code = (codes >> (3 * s)) & 7;
+      double cs = 0.0, cl = 0.0, cr = 0.0;
+      if (code & 4) {
+        double ls = we[0];
+#pragma unroll
+        for (int k = 1; k < NE; ++k) ls += we[k];
+        double mu = 0.0;  // adjoint of hm
+#pragma unroll
+        for (int k = 0; k < NE; ++k) mu = fma(args.lc.rce[k], we[k], mu);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) mu = fma(args.lc.rco[k], wo[k], mu);
+        const int br = code & 3;
+        cs = ls;
+        if (br == 2) {
+          cs -= mu;
+          cr = mu;
+        }
+        if (br == 3) {
+          cs += mu;
+          cl = -mu;
+        }
+        const double g = (br == 1) ? 2.0 * mu : 0.0;
+#pragma unroll
+        for (int k = 0; k < NE; ++k)
+          we[k] = g * fma(args.lc.dv0, args.lc.a0e[k], args.lc.dv1 * args.lc.a1e[k]);
+#pragma unroll
+        for (int k = 0; k < NO; ++k)
+          wo[k] = g * fma(args.lc.dv0, args.lc.a0o[k], args.lc.dv1 * args.lc.a1o[k]);
+      }
+      lds[CL + lane + 1] = cl;
+      lds[CR + lane + 1] = cr;
+      __syncthreads();
+      // Received: the left neighbour's cr and the right neighbour's cl; at a trajectory's
+      // ends the replicated neighbour average is the cell's own (SlopeLimitN.m:18).
+      const double alpha = cs + lds[EDGE && E.first ? CL + lane + 1 : CR + lane] +
+                           lds[EDGE && E.last ? CR + lane + 1 : CL + lane + 2];
+      const double av = alpha * args.lc.V00;
+#pragma unroll
+      for (int k = 0; k < NE; ++k) we[k] = fma(av, args.lc.a0e[k], we[k]);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) wo[k] = fma(av, args.lc.a0o[k], wo[k]);
+    }
+    const int f0 = (ss & 1) * 2 * (T + 2), f1 = f0 + (T + 2);
+    double qe[NE], qo[NO];
+    double gd = 0.0, gs = 0.0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      lre[k] = fma(RK<5>::B(s), we[k], lre[k]);
+      qe[k] = UNI ? lre[k] : sc * lre[k];
+      gd = fma(args.op.le[k], qe[k], gd);
+    }
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      lro[k] = fma(RK<5>::B(s), wo[k], lro[k]);
+      qo[k] = UNI ? lro[k] : sc * lro[k];
+      gs = fma(args.op.lo[k], qo[k], gs);
+    }
+    const double g0 = gd + gs;  // adjoints of du0 and du1
+    double g1 = gs - gd;
+    if constexpr (EDGE) g1 = E.last ? 0.0 : g1;
+    lds[f0 + lane + 1] = g0;
+    lds[f1 + lane + 1] = g1;
+    __builtin_amdgcn_sched_barrier(0);
+    double pe[NE], po[NO];  // transposed volume term: the adjoint of the flux values
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      double t = args.op.Qoe[j] * qo[0];
+#pragma unroll
+      for (int k = 1; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[k], t);
+      pe[j] = t;
+    }
+#pragma unroll
+    for (int j = 0; j < NO; ++j) {
+      double t = args.op.Qeo[j] * qe[0];
+#pragma unroll
+      for (int k = 1; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[k], t);
+      po[j] = t;
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) lre[k] = RK<5>::A(s) * lre[k];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) lro[k] = RK<5>::A(s) * lro[k];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) pin(pe[k]);
+#pragma unroll
+    for (int k = 0; k < NO; ++k) pin(po[k]);
+    __syncthreads();
+    const double gl = lds[EDGE && E.first ? CB + 6 : f1 + lane];
+    const double gr = lds[EDGE && E.last ? CB + 6 : f0 + lane + 2];
+    pe[0] += (g0 + g1) - (gr + gl);
+    po[0] += (g0 - g1) + (gr - gl);
+    if constexpr (BURG) {  // f'(u) = u: the symmetric block [[e, o], [o, e]] per node pair
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        const double e = se[s][k], o = so[s][k];
+        we[k] = fma(e, pe[k], fma(o, po[k], we[k]));
+        wo[k] = fma(o, pe[k], fma(e, po[k], wo[k]));
+      }
+      if constexpr (NE > NO) we[NO] = fma(se[s][NO], pe[NO], we[NO]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NE; ++k) we[k] += pe[k];
+#pragma unroll
+      for (int k = 0; k < NO; ++k) wo[k] += po[k];
+    }
+  }
+
+  if (args.has_eta && E.valid) eta[E.e] += eacc;
+  __syncthreads();  // the last stage's face reads are done before the image is rewritten
+  put_interior<NP, H>(lds, we, wo, true);
+  __syncthreads();
+  const int64_t o0 = tile * TE * NP;
+  if constexpr (EDGE) {
+    const int64_t rem = nd - o0;
+    store_run<T>(wout, o0, rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP, lds);
+  } else {
+    store_full<TE * NP, T>(wout, o0, lds);
+  }
+}
+
+template <int NP, bool BURG, bool LIM, bool UNI>
+__global__ __launch_bounds__(kBlock) void k_adj_nl(const double* __restrict__ win,
+                                                   double* __restrict__ wout,
+                                                   const double* __restrict__ snap,
+                                                   double* __restrict__ eta,
+                                                   const double* __restrict__ scale,
+                                                   NLAdjArgs<NP> args) {
+  constexpr int T = kBlock, H = 10 * cone_per_stage<LIM>();
+  __shared__ __attribute__((aligned(16))) double lds[NLGeo<NP>::kLds + 7];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  const int64_t e0 = tile * (T - 2 * H) - H;
+  if (edge_tile(e0, T, args.ktot, args.K))
+    nl_adj_tile<NP, BURG, LIM, UNI, true>(lds, tile, win, wout, snap, eta, scale, args);
+  else
+    nl_adj_tile<NP, BURG, LIM, UNI, false>(lds, tile, win, wout, snap, eta, scale, args);
+}
+
+// ---------------------------------------------------------------------------
+// Burgers RHS (parity entry point): one element per thread, global neighbour reads.
+// ---------------------------------------------------------------------------
+template <int NP>
+__global__ __launch_bounds__(kBlock) void k_rhs_nl(const double* __restrict__ u,
+                                                   double* __restrict__ rhs,
+                                                   const double* __restrict__ scale,
+                                                   OpArgs<NP> op, double s_uni, double fin,
+                                                   int64_t ktot, int32_t K) {
+  const int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (e >= ktot) return;
+  const int32_t kl = int32_t(e % K);
+  const bool first = (kl == 0), last = (kl == K - 1);
+  double f[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const double v = u[e * NP + i];
+    f[i] = 0.5 * v * v;
+  }
+  double fL = fin;
+  if (!first) {
+    const double v = u[(e - 1) * NP + NP - 1];
+    fL = 0.5 * v * v;
+  }
+  const double du0 = f[0] - fL;
+  double du1 = 0.0;
+  if (!last) {
+    const double v = u[(e + 1) * NP];
+    du1 = f[NP - 1] - 0.5 * v * v;
+  }
+  const double s = scale ? scale[kl] : s_uni;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    double t = op.L0[i] * du0;
+    t = fma(op.L1[i], du1, t);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) t = fma(op.Dm[i * NP + j], f[j], t);
+    rhs[e * NP + i] = s * t;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_src_copy(const double* __restrict__ w,
+                                                     const double* __restrict__ u, double c,
+                                                     double* __restrict__ out, int64_t n) {
+  const int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) out[i] = fma(c, u[i], w[i]);
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+template <int NP> LimEO<NP> make_lim_eo(const dg_plan* p) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  LimEO<NP> c;
+  const double* i0 = p->invV;       // row 1 of invV
+  const double* i1 = p->invV + NP;  // row 2
+  for (int k = 0; k < NO; ++k) {
+    c.a0e[k] = i0[k] + i0[N - k];
+    c.a0o[k] = i0[k] - i0[N - k];
+    c.a1e[k] = i1[k] + i1[N - k];
+    c.a1o[k] = i1[k] - i1[N - k];
+    c.rce[k] = 0.25 * (p->r[k] + p->r[N - k]);
+    c.rco[k] = 0.25 * (p->r[k] - p->r[N - k]);
+  }
+  if (NE > NO) {
+    c.a0e[NO] = i0[NO];
+    c.a1e[NO] = i1[NO];
+    c.rce[NO] = 0.5 * p->r[NO];
+  }
+  c.V00 = p->V[0];
+  double d0 = 0.0, d1 = 0.0;
+  for (int l = 0; l < NP; ++l) {
+    d0 += p->Dr[l] * p->V[l * NP + 0];
+    d1 += p->Dr[l] * p->V[l * NP + 1];
+  }
+  c.dv0 = d0;
+  c.dv1 = d1;
+  return c;
+}
+
+inline double flux_value(bool burg, double u) { return burg ? 0.5 * u * u : u; }
+
+template <int NP, bool BURG, bool LIM, int MS>
+int launch_step_nl(const dg_plan* p, const double* in, double* snap, double* last,
+                   const double* times, double dt, hipStream_t st) {
+  NLStepArgs<NP, MS> a;
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  a.lc = make_lim_eo<NP>(p);
+  a.sc = dt;
+  for (int m = 0; m < MS; ++m)
+    for (int s = 0; s < 5; ++s)
+      a.fin[m * 5 + s] = flux_value(BURG, inflow_value(p, times[m] + RK<5>::C(s) * dt));
+  a.ktot = p->ktot;
+  a.stride = p->ktot * NP;
+  a.K = int32_t(p->K);
+  a.xcd = p->xcd_order;
+  constexpr int TE = kBlock - 2 * MS * 5 * cone_per_stage<LIM>();
+  const unsigned grid = grid_for(p->ktot, TE);
+  if (p->uniform)
+    hipLaunchKernelGGL((k_step_nl<NP, BURG, LIM, true, MS>), dim3(grid), dim3(kBlock), 0, st, in,
+                       snap, last, p->d_scale, a);
+  else
+    hipLaunchKernelGGL((k_step_nl<NP, BURG, LIM, false, MS>), dim3(grid), dim3(kBlock), 0, st,
+                       in, snap, last, p->d_scale, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+template <int NP, bool BURG, bool LIM>
+int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const double* snap,
+                  double* eta, double t_n, double src, double dt, hipStream_t st) {
+  NLAdjArgs<NP> a;
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  a.lc = make_lim_eo<NP>(p);
+  a.sc = dt;
+  for (int s = 0; s < 5; ++s) a.fin[s] = flux_value(BURG, inflow_value(p, t_n + RK<5>::C(s) * dt));
+  a.fin[5] = flux_value(BURG, inflow_value(p, t_n + dt));
+  a.src = src;
+  a.ktot = p->ktot;
+  a.K = int32_t(p->K);
+  a.has_eta = eta != nullptr;
+  a.xcd = p->xcd_order;
+  constexpr int TE = kBlock - 20 * cone_per_stage<LIM>();
+  const unsigned grid = grid_for(p->ktot, TE);
+  if (p->uniform)
+    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, true>), dim3(grid), dim3(kBlock), 0, st, win,
+                       wout, snap, eta, p->d_scale, a);
+  else
+    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, false>), dim3(grid), dim3(kBlock), 0, st, win,
+                       wout, snap, eta, p->d_scale, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+// (flux, limiter) combinations: Burgers + limiter, Burgers alone, linear + limiter (the
+// plain linear flux runs the k_step / k_adj kernels of dg_advec.hip).
+template <int NP>
+int step_np(const dg_plan* p, int ms, const double* in, double* snap, double* last,
+            const double* times, double dt, hipStream_t st) {
+  const bool burg = p->flux == DG_FLUX_BURGERS, lim = p->limiter != 0;
+  if (burg && lim)
+    return ms == 2 ? launch_step_nl<NP, true, true, 2>(p, in, snap, last, times, dt, st)
+                   : launch_step_nl<NP, true, true, 1>(p, in, snap, last, times, dt, st);
+  if (burg)
+    return ms == 2 ? launch_step_nl<NP, true, false, 2>(p, in, snap, last, times, dt, st)
+                   : launch_step_nl<NP, true, false, 1>(p, in, snap, last, times, dt, st);
+  return ms == 2 ? launch_step_nl<NP, false, true, 2>(p, in, snap, last, times, dt, st)
+                 : launch_step_nl<NP, false, true, 1>(p, in, snap, last, times, dt, st);
+}
+
+template <int NP>
+int adj_np(const dg_plan* p, const double* win, double* wout, const double* snap, double* eta,
+           double t_n, double src, double dt, hipStream_t st) {
+  const bool burg = p->flux == DG_FLUX_BURGERS, lim = p->limiter != 0;
+  if (burg && lim) return launch_adj_nl<NP, true, true>(p, win, wout, snap, eta, t_n, src, dt, st);
+  if (burg) return launch_adj_nl<NP, true, false>(p, win, wout, snap, eta, t_n, src, dt, st);
+  return launch_adj_nl<NP, false, true>(p, win, wout, snap, eta, t_n, src, dt, st);
+}
+
+int launch_nl_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
+                   const double* times, double dt, hipStream_t st) {
+  int rc = DG_OK;
+  DG_DISPATCH_NP(p->NP, rc = step_np<NP>(p, ms, in, snap, last, times, dt, st));
+  return rc;
+}
+
+// Steps per launch of the limited kernels: 1 or 2 (the cone is 10 elements per step).
+inline int chunk_nl(const dg_plan* p, int left) {
+  const int m = p->msteps >= 2 ? 2 : 1;
+  return m > left ? left : m;
+}
+
+}  // namespace
+
+namespace dgk {
+
+int nl_rhs(const dg_plan* p, const double* u, double* rhs, double t, hipStream_t st) {
+  const double fin = flux_value(true, inflow_value(p, t));
+  const unsigned grid = grid_for(p->ktot, kBlock);
+  const double* sc = p->uniform ? nullptr : p->d_scale;
+  DG_DISPATCH_NP(p->NP, hipLaunchKernelGGL((k_rhs_nl<NP>), dim3(grid), dim3(kBlock), 0, st, u,
+                                           rhs, sc, make_op<NP>(p), p->s_uniform, fin, p->ktot,
+                                           int32_t(p->K)));
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
+           hipStream_t st) {
+  const int64_t field = p->ktot * p->NP;
+  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt (One_code.mlx:139)
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  if (snapshots) {
+    if (snapshots != u)
+      HIP_TRY(hipMemcpyAsync(snapshots, u, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
+    for (int n = 0; n < nsteps;) {
+      const int m = chunk_nl(p, nsteps - n);
+      double* last = (n + m == nsteps && snapshots != u) ? u : nullptr;
+      const int rc = launch_nl_step(p, m, snapshots + int64_t(n) * field,
+                                    snapshots + int64_t(n + 1) * field, last, &tn[n], dt, st);
+      if (rc) return rc;
+      n += m;
+    }
+    return DG_OK;
+  }
+  int launches = 0;  // ping-pong u <-> scratch, landing the last launch in u
+  for (int n = 0; n < nsteps; n += chunk_nl(p, nsteps - n)) ++launches;
+  double* a = u;
+  double* b = p->d_scratch;
+  if (launches % 2 == 1) {
+    HIP_TRY(hipMemcpyAsync(b, a, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
+    std::swap(a, b);
+  }
+  for (int n = 0; n < nsteps;) {
+    const int m = chunk_nl(p, nsteps - n);
+    const int rc = launch_nl_step(p, m, a, nullptr, b, &tn[n], dt, st);
+    if (rc) return rc;
+    std::swap(a, b);
+    n += m;
+  }
+  return DG_OK;
+}
+
+int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,
+           double src_coef, double* eta, hipStream_t st) {
+  const int64_t field = p->ktot * p->NP;
+  std::vector<double> tn(size_t(nsteps) + 1);
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  // Launch for step n reads w^{n+1} and u^n and writes w^n; intermediate states alternate
+  // between the plan scratch fields and the last launch lands in w.  (w may alias the
+  // terminal snapshot: only the first launch reads w, and no launch reads snapshot nsteps.)
+  const double* in = w;
+  int l = 0;
+  for (int n = nsteps - 1; n >= 0; --n, ++l) {
+    double* out = (n == 0 && nsteps > 1) ? w : ((l % 2 == 0) ? p->d_scratch : p->d_scratch2);
+    const double src = (n + 1 == nsteps) ? 0.0 : src_coef;  // left-endpoint rule
+    int rc = DG_OK;
+    DG_DISPATCH_NP(p->NP, rc = adj_np<NP>(p, in, out, snapshots + int64_t(n) * field, eta, tn[n],
+                                          src, dt, st));
+    if (rc) return rc;
+    in = out;
+  }
+  // Node-0 source w^0 += src u^0 (and the hand-back of a single-launch sweep).
+  if ((src_coef != 0.0 && nsteps > 0) || in != w) {
+    hipLaunchKernelGGL(k_src_copy, dim3(grid_for(field, kBlock)), dim3(kBlock), 0, st, in,
+                       snapshots, nsteps > 0 ? src_coef : 0.0, w, field);
+    HIP_TRY(hipGetLastError());
+  }
+  return DG_OK;
+}
+
+}  // namespace dgk

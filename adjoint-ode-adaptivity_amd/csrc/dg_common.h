@@ -1,0 +1,452 @@
+// dg_common.h — internals shared by the HIP translation units of libdgadv.so
+// (dg_advec.hip: linear-flux kernels + the C ABI; dg_burgers.hip: nonlinear flux and the
+// per-stage limiter).  Not part of the ABI: include/dg_advec.h is.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "dg_advec.h"
+
+namespace dgk {
+
+constexpr int kBlock = 256;       // lanes per workgroup = elements per tile (incl. halo)
+constexpr int kMaxNP = 9;         // N <= 8
+constexpr int kArgmaxParts = 1024;
+
+// Sets the calling thread's dg_last_error() text and returns `code` (dg_advec.hip).
+int fail(int code, const std::string& msg);
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess)                                                          \
+      return ::dgk::fail(DG_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));  \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Low-storage RK coefficients, utils/Globals1D.m:19-34 (LSERK4) and forward Euler.
+// ---------------------------------------------------------------------------
+template <int NS> struct RK;
+template <> struct RK<5> {
+  __host__ __device__ static constexpr double A(int s) {
+    return s == 0 ? 0.0
+         : s == 1 ? -567301805773.0 / 1357537059087.0
+         : s == 2 ? -2404267990393.0 / 2016746695238.0
+         : s == 3 ? -3550918686646.0 / 2091501179385.0
+                  : -1275806237668.0 / 842570457699.0;
+  }
+  __host__ __device__ static constexpr double B(int s) {
+    return s == 0 ? 1432997174477.0 / 9575080441755.0
+         : s == 1 ? 5161836677717.0 / 13612068292357.0
+         : s == 2 ? 1720146321549.0 / 2090206949498.0
+         : s == 3 ? 3134564353537.0 / 4481467310338.0
+                  : 2277821191437.0 / 14882151754819.0;
+  }
+  __host__ __device__ static constexpr double C(int s) {
+    return s == 0 ? 0.0
+         : s == 1 ? 1432997174477.0 / 9575080441755.0
+         : s == 2 ? 2526269341429.0 / 6820363962896.0
+         : s == 3 ? 2006345519317.0 / 3224310063776.0
+                  : 2802321613138.0 / 2924317926251.0;
+  }
+};
+template <> struct RK<1> {
+  __host__ __device__ static constexpr double A(int) { return 0.0; }
+  __host__ __device__ static constexpr double B(int) { return 1.0; }
+  __host__ __device__ static constexpr double C(int) { return 0.0; }
+};
+
+// Element operator, folded with the advection speed (host side, per plan):
+//   rhs_i = s_k * ( sum_j Dm[i][j] u_j + L0[i]*(u_0 - uL) + L1[i]*(u_N - uR) )
+//   Dm = -a*Dr, L0 = (-a/2)*LIFT(:,1), L1 = (a/2)*LIFT(:,2), s_k = rx = Fscale = 2/h_k.
+template <int NP> struct OpArgs {
+  double Dm[NP * NP];
+  double L0[NP];
+  double L1[NP];
+};
+
+// The same operator in even/odd node coordinates.  LGL nodes are symmetric about 0, so
+// with J the node-reversal matrix J*Dr*J = -Dr and LIFT(:,2) = J*LIFT(:,1).  Per element
+//   e_k = (u_k + u_{N-k})/2,  o_k = (u_k - u_{N-k})/2   (k < NO),   e_NO = u_mid (Np odd)
+// and the element operator splits into an odd->even and an even->odd block:
+//   rhs_e = Qeo o + le*(du0 - du1),   rhs_o = Qoe e + lo*(du0 + du1)
+// which is 2*NE*NO + NP fused multiply-adds per stage instead of NP*NP + 2*NP.
+// The blocks are built and checked on the host (make_eo).
+template <int NP> struct EOArgs {
+  static constexpr int NE = (NP + 1) / 2;
+  static constexpr int NO = NP / 2;
+  double Qeo[NE * NO];  // rhs_e[k] += Qeo[k*NO + j] * o[j]
+  double Qoe[NO * NE];  // rhs_o[k] += Qoe[k*NE + j] * e[j]
+  double le[NE];
+  double lo[NO];
+};
+
+// ---------------------------------------------------------------------------
+// Tile staging helpers.  A tile is the contiguous range of doubles of kBlock
+// consecutive elements starting at element e0 (which may be negative or run past
+// the end: those doubles read as 0 and are never used by a valid lane).
+// ---------------------------------------------------------------------------
+template <int NP>
+__device__ __forceinline__ int load_tile(const double* __restrict__ g, int64_t e0, int64_t nd,
+                                         double* __restrict__ lds) {
+  const int64_t d0 = e0 * NP;
+  const int64_t base = d0 & ~int64_t(1);           // 16-byte aligned start
+  const int off = int(d0 - base);                  // 0 or 1
+  const int nvec = (kBlock * NP + off + 1) >> 1;   // double2 count
+  const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
+  for (int v = threadIdx.x; v < nvec; v += kBlock) {
+    const int64_t gd = base + 2 * int64_t(v);
+    double2 val;
+    if (gd >= 0 && gd + 1 < nd) {
+      val = g2[gd >> 1];
+    } else {
+      val.x = (gd >= 0 && gd < nd) ? g[gd] : 0.0;
+      val.y = (gd + 1 >= 0 && gd + 1 < nd) ? g[gd + 1] : 0.0;
+    }
+    *reinterpret_cast<double2*>(&lds[2 * v]) = val;
+  }
+  return off;
+}
+
+// ---------------------------------------------------------------------------
+// Tile geometry of the fused step kernels.  A workgroup of LB = 256*W lanes owns a tile
+// of T = LB consecutive elements, one element per lane, its state in VGPRs.  The
+// dependency cone of one step is NS elements per side, so of MS fused steps the
+// TE = T - 2*MS*NS interior elements are exact and written back.  W = 2 halves the
+// redundant halo work (the kernels are fp64-VALU bound) at the same registers per lane.
+// ---------------------------------------------------------------------------
+template <int NP, int W> struct TileGeo {
+  static constexpr int LB = kBlock * W;
+  static constexpr int T = LB;
+  static constexpr int kVec = (T * NP + 2 + 2 * LB - 1) / (2 * LB);  // double2 / lane
+  static constexpr int kTileD = T * NP + 2;  // staging image (+2: 16-byte realignment)
+  static constexpr int kFaceD = 4 * (T + 2);  // 2 double-buffered face arrays, padded by 1
+  static constexpr int kLds = kTileD > kFaceD ? kTileD : kFaceD;
+};
+
+// Issue the 16-byte loads of one tile image into registers (coalesced: lane-consecutive
+// double2), then commit them to LDS.  Elements outside [0, ktot) read as zero.
+template <int NP, int W> struct TileRegs {
+  double2 v[TileGeo<NP, W>::kVec];
+  int off;
+};
+
+template <int NP, int W, bool EDGE = true>
+__device__ __forceinline__ void tile_issue(const double* __restrict__ g, int64_t e0, int64_t nd,
+                                           TileRegs<NP, W>& r) {
+  using G = TileGeo<NP, W>;
+  const int64_t d0 = e0 * NP;
+  const int64_t base = d0 & ~int64_t(1);
+  r.off = int(d0 - base);
+  const int nvec = (G::T * NP + r.off + 1) >> 1;
+  const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = threadIdx.x + q * G::LB;
+    const int64_t gd = base + 2 * int64_t(v);
+    double2 val = make_double2(0.0, 0.0);
+    if (v < nvec) {
+      if (!EDGE || (gd >= 0 && gd + 1 < nd)) {  // interior tiles: always in range
+        val = g2[gd >> 1];
+      } else {
+        if (gd >= 0 && gd < nd) val.x = g[gd];
+        if (gd + 1 >= 0 && gd + 1 < nd) val.y = g[gd + 1];
+      }
+    }
+    r.v[q] = val;
+  }
+}
+
+template <int NP, int W>
+__device__ __forceinline__ void tile_commit(const TileRegs<NP, W>& r, double* __restrict__ lds) {
+  using G = TileGeo<NP, W>;
+  const int nvec = (G::T * NP + r.off + 1) >> 1;
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = threadIdx.x + q * G::LB;
+    if (v < nvec) *reinterpret_cast<double2*>(&lds[2 * v]) = r.v[q];
+  }
+}
+
+// Store `count` doubles from lds[0..count) to g[o0..o0+count); o0 must be even.
+template <int LB = kBlock>
+__device__ __forceinline__ void store_run(double* __restrict__ g, int64_t o0, int64_t count,
+                                          const double* __restrict__ lds) {
+  double2* __restrict__ g2 = reinterpret_cast<double2*>(g);
+  for (int64_t v = threadIdx.x; 2 * v < count; v += LB) {
+    const double2 val = *reinterpret_cast<const double2*>(&lds[2 * v]);
+    const int64_t gd = o0 + 2 * v;
+    if (2 * v + 1 < count) {
+      g2[gd >> 1] = val;
+    } else {
+      g[gd] = val.x;
+    }
+  }
+}
+
+// Store a full tile output (COUNT doubles, compile-time) from lds to g[o0..); o0 even.
+template <int COUNT, int LB>
+__device__ __forceinline__ void store_full(double* __restrict__ g, int64_t o0,
+                                           const double* __restrict__ lds) {
+  static_assert(COUNT % 2 == 0, "16-byte runs");
+  constexpr int NV = COUNT / 2, NQ = (NV + LB - 1) / LB;
+  double2* __restrict__ g2 = reinterpret_cast<double2*>(g + o0);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int v = int(threadIdx.x) + q * LB;
+    if ((q + 1) * LB <= NV || v < NV) g2[v] = *reinterpret_cast<const double2*>(&lds[2 * v]);
+  }
+}
+
+// A tile is an edge tile when its element range [e0, e0+T) leaves [0, ktot) or contains
+// a trajectory's first or last element (uniform per workgroup).  Interior tiles -- all
+// but a handful -- run a specialisation without inflow/outflow selects or bounds checks.
+__device__ __forceinline__ bool edge_tile(int64_t e0, int T, int64_t ktot, int32_t K) {
+  if (e0 < 0 || e0 + T > ktot) return true;
+  const int64_t kl0 = int64_t(uint32_t(e0) % uint32_t(K));
+  return kl0 == 0 || kl0 + T >= K;
+}
+
+// Per-element geometry: global element e = e0 + el, position kl inside its trajectory.
+struct Elem {
+  int64_t e;
+  int32_t kl;
+  bool inrange, first, last, valid;
+};
+
+template <int H, int T, bool EDGE = true>
+__device__ __forceinline__ Elem elem_info(int64_t e0, int el, int64_t ktot, int32_t K) {
+  Elem E;
+  E.e = e0 + el;
+  if constexpr (!EDGE) {
+    E.kl = int32_t(uint32_t(E.e) % uint32_t(K));
+    E.inrange = true;
+    E.first = E.last = false;
+    E.valid = el >= H && el < T - H;
+    return E;
+  }
+  E.inrange = (E.e >= 0 && E.e < ktot);
+  // ktot < 2^31 (checked at plan creation): 32-bit division.
+  E.kl = E.inrange ? int32_t(uint32_t(E.e) % uint32_t(K)) : 0;
+  E.first = (E.kl == 0);
+  E.last = (E.kl == K - 1);
+  E.valid = E.inrange && el >= H && el < T - H;
+  return E;
+}
+
+// Tile of workgroup b.  The dispatcher deals workgroups round-robin over the 8 XCDs
+// (b, b+8, ... share one; cdna_hip_programming.md §5.5 T1), so giving each XCD a
+// contiguous range of tiles makes neighbouring tiles -- which re-read each other's halo
+// lines -- run on one L2.  Bijective for any n; a speed choice only.
+__device__ __forceinline__ int64_t tile_of(int64_t b, int64_t n, bool xcd) {
+  if (!xcd || n < 16) return b;
+  const int64_t q = n / 8, r = n % 8, x = b % 8, j = b / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
+
+// Boundary handling in the face exchange is done by *index* selection into LDS (one
+// 32-bit v_cndmask), never by value/pointer selection: `c ? kernarg : lds[i]` lets the
+// compiler fold a select of pointers into a flat load on every stage's critical path.
+// Each kernel keeps its per-stage boundary constants (inflow values, a zero) in a few
+// doubles at the end of its LDS array, written by edge tiles only.
+
+// Materialise a value at this point of the program: an empty volatile asm keeps its
+// order with the barrier, so work placed before a __syncthreads() is not sunk below it by
+// the IR optimisers (the machine scheduler never moves code across s_barrier).
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+
+// Even/odd element state helpers.
+template <int NP>
+__device__ __forceinline__ void to_eo(const double* u, double* ev, double* od) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    ev[k] = 0.5 * (u[k] + u[N - k]);
+    od[k] = 0.5 * (u[k] - u[N - k]);
+  }
+  if constexpr (NE > NO) ev[NO] = u[NO];
+}
+
+template <int NP>
+__device__ __forceinline__ void from_eo(const double* ev, const double* od, double* u) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    u[k] = ev[k] + od[k];
+    u[N - k] = ev[k] - od[k];
+  }
+  if constexpr (NE > NO) u[NO] = ev[NO];
+}
+
+// Write the TE interior elements of the tile (element-major, nodal) through the LDS
+// image with 16-byte stores.  Callers barrier before (face reads done) and after (when
+// the image is reused).
+template <int NP, int W, int H>
+__device__ __forceinline__ void stage_out(double* __restrict__ lds, const double (*ev)[(NP + 1) / 2],
+                                          const double (*od)[NP / 2], bool dual) {
+  constexpr int T = TileGeo<NP, W>::T, EPL = 1;
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int m = 0; m < EPL; ++m) {
+    const int el = m * T + lane;
+    if (el >= H && el < T - H) {
+      double* o = lds + (el - H) * NP;
+      if (dual) {  // dual coordinates back to nodal: w_k = (we+wo)/2, w_{N-k} = (we-wo)/2
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          o[k] = 0.5 * (ev[m][k] + od[m][k]);
+          o[N - k] = 0.5 * (ev[m][k] - od[m][k]);
+        }
+        if constexpr (NE > NO) o[NO] = ev[m][NO];
+      } else {
+        from_eo<NP>(ev[m], od[m], o);
+      }
+    }
+  }
+}
+
+}  // namespace dgk
+
+// ---------------------------------------------------------------------------
+// Plan
+// ---------------------------------------------------------------------------
+struct dg_plan {
+  int N = 0, NP = 0;
+  int64_t K = 0, batch = 0, ktot = 0;
+  int64_t K_cap = 0;  // elements per trajectory the device buffers hold (dg_plan_reserve)
+  double a = 0.0;
+  int inflow = 0, scheme = 0, nstages = 5;
+  bool uniform = true;
+  double s_uniform = 0.0;  // 2/h for uniform meshes
+  double r[dgk::kMaxNP], V[dgk::kMaxNP * dgk::kMaxNP], invV[dgk::kMaxNP * dgk::kMaxNP],
+      Dr[dgk::kMaxNP * dgk::kMaxNP],
+      LIFT[dgk::kMaxNP * 2];
+  double* d_scale = nullptr;  // K_cap: 2/h_k
+  double* d_VX = nullptr;     // K_cap+1
+  double* d_scratch = nullptr;   // two fields: adjoint ping-pong lands the last launch in w
+  double* d_scratch2 = nullptr;
+  double* d_pv = nullptr;
+  int64_t* d_pi = nullptr;
+  // tuning (dg_plan_tune): tile width of the step kernels (tile = 256*tile_width elements)
+  int tile_width = 1;
+  int msteps = 4;  // time steps fused per launch (1, 2 or 4)
+  int xcd_order = 1;  // XCD-aware tile order
+  // physics (dg_plan_set_physics): DG_FLUX_LINEAR / DG_FLUX_BURGERS, SlopeLimitN per stage
+  int flux = 0;
+  int limiter = 0;
+  bool nonlinear() const { return flux != 0 || limiter != 0; }
+};
+
+namespace dgk {
+
+inline double inflow_value(const dg_plan* p, double t) {
+  return (p->inflow == DG_INFLOW_SIN_A2T) ? -std::sin(p->a * p->a * t) : -std::sin(p->a * t);
+}
+
+// scale = 1 gives the plain operator (rhs); the steppers fold dt*2/h into it on uniform meshes.
+template <int NP> OpArgs<NP> make_op(const dg_plan* p, double scale = 1.0) {
+  OpArgs<NP> op;
+  for (int i = 0; i < NP; ++i) {
+    for (int j = 0; j < NP; ++j) op.Dm[i * NP + j] = scale * (-p->a * p->Dr[i * NP + j]);
+    op.L0[i] = scale * ((-p->a / 2.0) * p->LIFT[i * 2 + 0]);
+    op.L1[i] = scale * ((p->a / 2.0) * p->LIFT[i * 2 + 1]);
+  }
+  return op;
+}
+
+// Even/odd blocks of the element operator (see EOArgs).  Returns false if the operator
+// is not centro-(anti)symmetric to 1e-12, i.e. the nodes are not symmetric.
+template <int NP> bool make_eo(const dg_plan* p, double scale, EOArgs<NP>* out) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  double Dm[NP][NP], L0[NP], L1[NP], T[NP][NP] = {}, Ti[NP][NP] = {};
+  for (int i = 0; i < NP; ++i) {
+    for (int j = 0; j < NP; ++j) Dm[i][j] = scale * (-p->a * p->Dr[i * NP + j]);
+    L0[i] = scale * ((-p->a / 2.0) * p->LIFT[i * 2 + 0]);
+    L1[i] = scale * ((p->a / 2.0) * p->LIFT[i * 2 + 1]);
+  }
+  for (int k = 0; k < NO; ++k) {  // rows: e_0..e_{NE-1}, o_0..o_{NO-1}
+    T[k][k] += 0.5; T[k][N - k] += 0.5;
+    T[NE + k][k] += 0.5; T[NE + k][N - k] -= 0.5;
+    Ti[k][k] += 1.0; Ti[k][NE + k] += 1.0;
+    Ti[N - k][k] += 1.0; Ti[N - k][NE + k] -= 1.0;
+  }
+  if (NE > NO) { T[NO][NO] = 1.0; Ti[NO][NO] = 1.0; }
+  double TD[NP][NP], Q[NP][NP], l0[NP], l1[NP];
+  for (int i = 0; i < NP; ++i)
+    for (int j = 0; j < NP; ++j) {
+      double t = 0.0;
+      for (int k = 0; k < NP; ++k) t += T[i][k] * Dm[k][j];
+      TD[i][j] = t;
+    }
+  double qmax = 0.0, lmax = 0.0;
+  for (int i = 0; i < NP; ++i) {
+    for (int j = 0; j < NP; ++j) {
+      double t = 0.0;
+      for (int k = 0; k < NP; ++k) t += TD[i][k] * Ti[k][j];
+      Q[i][j] = t;
+      qmax = std::fmax(qmax, std::fabs(t));
+    }
+    double a0 = 0.0, a1 = 0.0;
+    for (int k = 0; k < NP; ++k) {
+      a0 += T[i][k] * L0[k];
+      a1 += T[i][k] * L1[k];
+    }
+    l0[i] = a0;
+    l1[i] = a1;
+    lmax = std::fmax(lmax, std::fmax(std::fabs(a0), std::fabs(a1)));
+  }
+  bool ok = true;
+  const double tq = 1e-12 * qmax, tl = 1e-12 * lmax;
+  for (int i = 0; i < NE; ++i)
+    for (int j = 0; j < NE; ++j) ok = ok && std::fabs(Q[i][j]) <= tq;           // even->even
+  for (int i = 0; i < NO; ++i)
+    for (int j = 0; j < NO; ++j) ok = ok && std::fabs(Q[NE + i][NE + j]) <= tq;  // odd->odd
+  for (int k = 0; k < NE; ++k) ok = ok && std::fabs(l0[k] + l1[k]) <= tl;
+  for (int k = 0; k < NO; ++k) ok = ok && std::fabs(l0[NE + k] - l1[NE + k]) <= tl;
+  if (out) {
+    for (int k = 0; k < NE; ++k)
+      for (int j = 0; j < NO; ++j) out->Qeo[k * NO + j] = Q[k][NE + j];
+    for (int k = 0; k < NO; ++k)
+      for (int j = 0; j < NE; ++j) out->Qoe[k * NE + j] = Q[NE + k][j];
+    for (int k = 0; k < NE; ++k) out->le[k] = 0.5 * (l0[k] - l1[k]);
+    for (int k = 0; k < NO; ++k) out->lo[k] = 0.5 * (l0[NE + k] + l1[NE + k]);
+  }
+  return ok;
+}
+
+inline unsigned grid_for(int64_t n, int64_t per) { return unsigned((n + per - 1) / per); }
+
+// Dispatch on Np (2..9) and the number of stages.
+#define DG_DISPATCH_NP(NPV, CALL) \
+  switch (NPV) {                  \
+    case 2: { constexpr int NP = 2; CALL; } break; \
+    case 3: { constexpr int NP = 3; CALL; } break; \
+    case 4: { constexpr int NP = 4; CALL; } break; \
+    case 5: { constexpr int NP = 5; CALL; } break; \
+    case 6: { constexpr int NP = 6; CALL; } break; \
+    case 7: { constexpr int NP = 7; CALL; } break; \
+    case 8: { constexpr int NP = 8; CALL; } break; \
+    case 9: { constexpr int NP = 9; CALL; } break; \
+    default: return fail(DG_ERR_ARG, "unsupported Np"); \
+  }
+
+// Nonlinear-flux / per-stage-limiter steppers (dg_burgers.hip), dispatched from the C ABI
+// when plan->nonlinear().
+int nl_rhs(const dg_plan* p, const double* u, double* rhs, double t, hipStream_t st);
+int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
+           hipStream_t st);
+int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,
+           double src_coef, double* eta, hipStream_t st);
+
+}  // namespace dgk

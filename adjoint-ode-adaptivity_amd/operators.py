@@ -11,7 +11,12 @@ LSERK4 loop, One_code.mlx:106-140   ``op.forward(u, t0, dt, nsteps, snapshots)``
 ``err_contribution`` / errEst role  the ``eta`` output of ``op.adjoint``
 ``SlopeLimitN(u)``                  ``op.slope_limit(u)``      (utils/SlopeLimitN.m:1)
 ``argmax(err)`` (:337)              ``op.argmax(eta, use_abs=True)``
+split of :336-341 / MAIN.m:137-141  ``op.refine(idx)`` (on the device)
 =================================  ===============================================
+
+``flux="burgers"`` and/or ``limiter=True`` select the config-3 physics (BASELINE.json
+configs[2]): the build-defined flux a*u^2/2 with AdvecRHS1D's central-flux structure and
+SlopeLimitN after every LSERK4 stage (see include/dg_advec.h ``dg_plan_set_physics``).
 
 Tensors are torch CUDA float64 tensors in the device layout (element-major,
 ``u[(b*K + k)*Np + i]``); any shape with that many contiguous elements is accepted.
@@ -28,6 +33,7 @@ from .galerkin import BaseGalerkin1D
 
 INFLOW = {"a": _lib.DG_INFLOW_SIN_AT, "a2": _lib.DG_INFLOW_SIN_A2T}
 SCHEME = {"lserk4": _lib.DG_TIME_LSERK4, "euler": _lib.DG_TIME_EULER}
+FLUX = {"linear": _lib.DG_FLUX_LINEAR, "burgers": _lib.DG_FLUX_BURGERS}
 
 
 def _stream(device):
@@ -44,10 +50,12 @@ class DGAdvection1D:
     batch: independent trajectories (ensemble ICs) sharing the mesh.
     inflow: "a" (uin = -sin(a t), AdvecRHS1D.m:14) or "a2" (-sin(a^2 t), One_code.mlx:129).
     time_scheme: "lserk4" (Globals1D.m:19-34) or "euler".
+    flux: "linear" (a*u, AdvecRHS1D) or "burgers" (a*u^2/2, build-defined, config 3).
+    limiter: apply SlopeLimitN (utils/SlopeLimitN.m) after every LSERK4 stage.
   """
 
   def __init__(self, mesh, a=2 * np.pi, batch=1, inflow="a", time_scheme="lserk4",
-               v_x=None, device=None):
+               v_x=None, device=None, flux="linear", limiter=False):
     if not isinstance(mesh, BaseGalerkin1D):
       mesh = BaseGalerkin1D(n=int(mesh), v_x=v_x)
     if not torch.cuda.is_available():
@@ -73,12 +81,20 @@ class DGAdvection1D:
     _lib.check(rc, "dg_plan_create")
     self._plan = handle
     self._lib = lib
+    self.flux = flux
+    self.limiter = bool(limiter)
+    if flux != "linear" or limiter:
+      _lib.check(lib.dg_plan_set_physics(handle, FLUX[flux], int(bool(limiter))),
+                 "dg_plan_set_physics")
     self._query()
     self._idx = torch.zeros(1, dtype=torch.int64, device=self.device)
 
   def _query(self):
     q = (ctypes.c_int64 * 8)()
     _lib.check(self._lib.dg_plan_query(self._plan, q), "dg_plan_query")
+    self.K = int(q[2])
+    self.ktot = self.K * self.batch
+    self.field_numel = self.ktot * self.Np
     self.uniform = bool(q[4])
     self.stages = int(q[5])
     self.tile_width = int(q[6])
@@ -119,6 +135,37 @@ class DGAdvection1D:
                                         int(steps_per_launch)), "dg_plan_tune")
     self._query()
     return self
+
+  # --- mesh refinement on the device ---
+  def reserve(self, k_capacity):
+    """Size the plan's device buffers for meshes of up to ``k_capacity`` elements."""
+    _lib.check(self._lib.dg_plan_reserve(self._plan, int(k_capacity)), "dg_plan_reserve")
+    return self
+
+  def refine(self, idx, h_split=None):
+    """Split element ``idx`` (a 1-element CUDA int64 tensor, e.g. ``argmax_async``'s
+    output) at its midpoint on the device (Main_finite_difference.py:336-341,
+    MAIN.m:137-141).  K grows by one; fields of the old size must be re-initialised.
+    ``h_split`` (1-element CUDA float64, optional) receives the split element's width."""
+    if not isinstance(idx, torch.Tensor) or not idx.is_cuda or idx.dtype != torch.int64:
+      raise TypeError("idx must be a CUDA int64 tensor")
+    hp = None
+    if h_split is not None:
+      if not h_split.is_cuda or h_split.dtype != torch.float64:
+        raise TypeError("h_split must be a CUDA float64 tensor")
+      hp = ctypes.c_void_p(h_split.data_ptr())
+    rc = self._lib.dg_plan_refine(self._plan, ctypes.c_void_p(idx.data_ptr()), hp,
+                                  _stream(self.device))
+    _lib.check(rc, "dg_plan_refine")
+    self._query()
+    return self.K
+
+  def v_x(self):
+    """The plan's current vertex coordinates (host copy; synchronises)."""
+    out = np.empty(self.K + 1)
+    rc = self._lib.dg_plan_get_mesh(self._plan, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    _lib.check(rc, "dg_plan_get_mesh")
+    return out
 
   # --- checks ---
   def _field(self, t, name, numel=None, dtype=torch.float64):

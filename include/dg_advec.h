@@ -88,6 +88,39 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
+/* Physics of the plan's steppers.  Default: DG_FLUX_LINEAR + DG_LIMIT_NONE (AdvecRHS1D).
+ *   DG_FLUX_LINEAR      f(u) = a*u                               utils/AdvecRHS1D.m:9-19
+ *   DG_FLUX_BURGERS     f(u) = a*u^2/2 at the nodes with AdvecRHS1D's central-flux structure
+ *                       on f and inflow f(uin) (build-defined, BASELINE config 3, SURVEY 8d;
+ *                       CPU statement oracle/burgers.py)
+ *   DG_LIMIT_EACH_STAGE u = SlopeLimitN(u) (utils/SlopeLimitN.m:1-33) after every stage update
+ * Both need DG_TIME_LSERK4.  With either, dg_advec_rhs evaluates the flux's RHS (no limiter),
+ * dg_lserk4_fwd runs limited steps (at most 2 per launch), and dg_lserk4_adj is the exact
+ * transpose of each step's tangent at the stored forward states, with the limiter's discrete
+ * decisions (troubled cells, active minmod argument) frozen; it recomputes step n's stages from
+ * snapshots[n] (one launch per step) and takes the indicator residual of the flux f. */
+enum { DG_FLUX_LINEAR = 0, DG_FLUX_BURGERS = 1 };
+enum { DG_LIMIT_NONE = 0, DG_LIMIT_EACH_STAGE = 1 };
+int dg_plan_set_physics(dg_plan* plan, int flux, int limiter);
+
+/* Grow the plan's device mesh and scratch buffers to hold K_capacity elements per trajectory,
+ * so that dg_plan_refine can add elements without reallocating.  Synchronous (waits for the
+ * device); never shrinks; a no-op when the capacity suffices. */
+int dg_plan_reserve(dg_plan* plan, int64_t K_capacity);
+
+/* Refine on the device: split element idx[0] (device int64 in [0, K), e.g. dg_argmax's
+ * output) at its midpoint, i.e. insert 0.5*(VX[idx] + VX[idx+1]) after vertex idx — the split
+ * of python/Main_finite_difference.py:336-341 (ref_idx = argmax + 1) and matlab/MAIN.m:137-141 —
+ * with the new elements' metric 2/h as dg_plan_create computes it.  K grows by one and the
+ * mesh is non-uniform from then on; fields sized for the old K must be re-initialised by the
+ * caller (e.g. dg_init_sine).  h_split (nullable, device double) receives the width of the
+ * split element.  Needs K+1 <= capacity (dg_plan_reserve).  Asynchronous on stream; the plan
+ * is modified, so it must not be used concurrently. */
+int dg_plan_refine(dg_plan* plan, const int64_t* idx, double* h_split, void* stream);
+
+/* Copy the plan's current K+1 vertex coordinates to the host array VX (synchronous). */
+int dg_plan_get_mesh(const dg_plan* plan, double* VX);
+
 /* rhs = AdvecRHS1D(u, t, a)   — utils/AdvecRHS1D.m:1-20 (inline copy One_code.mlx:124-134).
  * Central flux (alpha = 1), inflow at each trajectory's x = 0, du = 0 at the outflow face. */
 int dg_advec_rhs(const dg_plan* plan, const double* u, double* rhs, double t, void* stream);

@@ -1,0 +1,292 @@
+"""Config-3 path on the GPU (Burgers-type flux, SlopeLimitN after every LSERK4 stage,
+frozen-decision adjoint, device-side refinement) vs the CPU oracle (oracle/burgers.py),
+through the C ABI.  Needs an MI355X.
+
+Tolerances: fp64 fields and indicators within RTOL = 1e-10 of max|oracle| (north_star);
+the device split of the mesh is bit-exact against the host split_interval.  As for the
+linear path, the adjoint/indicator oracle is fed the GPU's own forward snapshots.
+"""
+import numpy as np
+import pytest
+
+from oracle import adjoint as oadj
+from oracle import advec as oadv
+from oracle import burgers as ob
+from oracle import setup1d
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-10
+A = 2 * np.pi
+PHYSICS = [("burgers", True), ("burgers", False), ("linear", True)]
+
+
+def rel_err(x, ref):
+  x, ref = np.asarray(x), np.asarray(ref)
+  return float(np.max(np.abs(x - ref)) / max(np.max(np.abs(ref)), 1e-300))
+
+
+def dev(x, device):
+  import torch
+  return torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=device)
+
+
+def host(t):
+  return t.detach().cpu().numpy()
+
+
+def setup(pkg, N, K, v_x=None, **kw):
+  if v_x is None:
+    _, v_x, _, _ = setup1d.mesh_gen1d(0.0, 1.0, K)
+  S = setup1d.startup1d(N, v_x, metric="element")
+  mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+  return S, mesh, pkg.operators.DGAdvection1D(mesh, **kw)
+
+
+def ic(S, rng, jump=0.8):
+  x = S["x"]
+  return np.sin(2 * np.pi * x) + jump * (x > 0.5) + 0.05 * rng.standard_normal(x.shape)
+
+
+def refined_vx(K, rng):
+  _, v_x, _, _ = setup1d.mesh_gen1d(0.0, 1.0, K)
+  for _ in range(7):
+    v_x = np.insert(v_x, (j := int(rng.integers(0, len(v_x) - 1))) + 1,
+                    0.5 * (v_x[j] + v_x[j + 1]))
+  return v_x
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("N", [1, 2, 4, 8])
+@pytest.mark.parametrize("inflow", ["a", "a2"])
+def test_burgers_rhs(pkg, gpu, N, inflow):
+  rng = np.random.default_rng(N)
+  S, mesh, op = setup(pkg, N, 333, flux="burgers", inflow=inflow)
+  u = rng.standard_normal((N + 1, 333))
+  ref, _ = ob.rhs(u, 0.37, A, S, ob.FLUX_BURGERS, inflow)
+  got = host(op.rhs(dev(setup1d.to_elem_major(u), gpu), 0.37))
+  assert rel_err(setup1d.from_elem_major(got, N + 1), ref) <= RTOL
+
+
+def test_burgers_rhs_nonuniform(pkg, gpu):
+  rng = np.random.default_rng(3)
+  v_x = refined_vx(200, rng)
+  S, mesh, op = setup(pkg, 3, None, v_x=v_x, flux="burgers")
+  assert not op.uniform
+  u = rng.standard_normal((4, len(v_x) - 1))
+  ref, _ = ob.rhs(u, 0.1, A, S)
+  got = host(op.rhs(dev(setup1d.to_elem_major(u), gpu), 0.1))
+  assert rel_err(setup1d.from_elem_major(got, 4), ref) <= RTOL
+
+
+@pytest.mark.parametrize("flux,limit", PHYSICS)
+@pytest.mark.parametrize("N,K,uniform", [(4, 300, True), (2, 257, True), (7, 150, True),
+                                         (3, 240, False)])
+def test_limited_forward_sweep(pkg, gpu, flux, limit, N, K, uniform):
+  rng = np.random.default_rng(N * 1000 + K)
+  v_x = None if uniform else refined_vx(K, rng)
+  S, mesh, op = setup(pkg, N, K, v_x=v_x, flux=flux, limiter=limit)
+  u0 = ic(S, rng)
+  dt = oadv.bench_dt(S)
+  nsteps = 5  # 2 + 2 + 1 steps per launch
+  ref, _ = ob.forward_sweep(u0, 0.02, dt, nsteps, A, S, flux, limit=limit)
+  if limit:
+    counts = ob.limiter_stage_ids(u0, 0.02, dt, 1, A, S, flux)
+    assert min(counts[0]) > 0  # the limiter is active
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  snaps = op.new_field(nsteps + 1)
+  op.forward(u, 0.02, dt, nsteps, snaps)
+  for n in range(nsteps + 1):
+    assert rel_err(setup1d.from_elem_major(host(snaps[n]), N + 1), ref[n]) <= RTOL, n
+  np.testing.assert_array_equal(host(u), host(snaps[nsteps]))
+  # ping-pong path (no snapshots) and one step per launch
+  u2 = dev(setup1d.to_elem_major(u0), gpu)
+  op.forward(u2, 0.02, dt, nsteps)
+  np.testing.assert_array_equal(host(u2), host(snaps[nsteps]))
+  op.tune(steps_per_launch=1)
+  u3 = dev(setup1d.to_elem_major(u0), gpu)
+  op.forward(u3, 0.02, dt, nsteps)
+  assert rel_err(host(u3), host(u2)) <= 1e-12
+
+
+@pytest.mark.parametrize("flux,limit", PHYSICS)
+@pytest.mark.parametrize("N,K,uniform", [(3, 70, True), (4, 45, False)])
+def test_adjoint_sweep_and_indicator(pkg, gpu, flux, limit, N, K, uniform):
+  import torch
+  rng = np.random.default_rng(K + N)
+  v_x = None if uniform else refined_vx(K, rng)
+  S, mesh, op = setup(pkg, N, K, v_x=v_x, flux=flux, limiter=limit)
+  K = S["K"]
+  u0 = ic(S, rng)
+  dt = oadv.bench_dt(S)
+  nsteps, src = 3, 0.6
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  snaps = op.new_field(nsteps + 1)
+  op.forward(u, 0.01, dt, nsteps, snaps)
+  times = [0.01]
+  for _ in range(nsteps):
+    times.append(times[-1] + dt)
+  gsnaps = [setup1d.from_elem_major(host(snaps[n]), N + 1) for n in range(nsteps + 1)]
+  g = rng.standard_normal(u0.shape)
+  w_ref, eta_ref, _ = ob.adjoint_sweep(g, gsnaps, times, dt, A, S, flux, limit=limit,
+                                       src_coef=src)
+  w = dev(setup1d.to_elem_major(g), gpu)
+  eta = torch.zeros(K, dtype=torch.float64, device=gpu)
+  op.adjoint(w, snaps, 0.01, dt, nsteps, src_coef=src, eta=eta)
+  assert rel_err(setup1d.from_elem_major(host(w), N + 1), w_ref) <= RTOL
+  assert rel_err(host(eta), eta_ref) <= RTOL
+
+
+@pytest.mark.parametrize("limit", [False, True])
+def test_gradient_matches_finite_difference(pkg, gpu, limit):
+  """dJ/du0 through 4 limited Burgers steps vs a central difference of J on the GPU
+  (matlab/test_jacobian.m:38-55 method).  With the limiter the step is only piecewise
+  smooth: its troubled-cell test compares against eps0 = 1e-8 (SlopeLimitN.m:23), so the
+  difference step must stay far below that for no decision to flip (h = 1e-10, and a
+  looser tolerance for the rounding of the difference quotient)."""
+  import torch
+  rng = np.random.default_rng(11)
+  S, mesh, op = setup(pkg, 4, 400, flux="burgers", limiter=limit)
+  u0 = dev(setup1d.to_elem_major(ic(S, rng)), gpu)
+  d = dev(rng.standard_normal(5 * 400), gpu)
+  g = dev(rng.standard_normal(5 * 400), gpu)
+  dt = oadv.bench_dt(S)
+  nsteps, src = 4, 0.3
+
+  def J(x):
+    snaps = op.new_field(nsteps + 1)
+    op.forward(x.clone(), 0.0, dt, nsteps, snaps)
+    val = float(torch.dot(g, snaps[nsteps]))
+    for n in range(nsteps):
+      val += 0.5 * src * float(torch.dot(snaps[n], snaps[n]))
+    return val, snaps
+
+  _, snaps = J(u0)
+  w = g.clone()
+  op.adjoint(w, snaps, 0.0, dt, nsteps, src_coef=src)
+  h, tol = (1e-10, 1e-5) if limit else (1e-6, 1e-7)
+  fd = (J(u0 + h * d)[0] - J(u0 - h * d)[0]) / (2 * h)
+  ad = float(torch.dot(w, d))
+  assert abs(fd - ad) <= tol * abs(ad)
+
+
+def test_adjoint_in_place_on_terminal_snapshot(pkg, gpu):
+  import torch
+  rng = np.random.default_rng(12)
+  S, mesh, op = setup(pkg, 4, 500, flux="burgers", limiter=True)
+  u0 = dev(setup1d.to_elem_major(ic(S, rng)), gpu)
+  dt = oadv.bench_dt(S)
+  for nsteps in (1, 4):
+    snaps = op.new_field(nsteps + 1)
+    op.forward(u0.clone(), 0.0, dt, nsteps, snaps)
+    w = snaps[nsteps].clone()
+    e1 = torch.zeros(500, dtype=torch.float64, device=gpu)
+    op.adjoint(w, snaps, 0.0, dt, nsteps, eta=e1)
+    e2 = torch.zeros(500, dtype=torch.float64, device=gpu)
+    op.adjoint(snaps[nsteps], snaps, 0.0, dt, nsteps, eta=e2)
+    np.testing.assert_array_equal(host(snaps[nsteps]), host(w))
+    np.testing.assert_array_equal(host(e1), host(e2))
+
+
+# ---------------------------------------------------------------------------
+def test_device_refine_is_the_host_split(pkg, gpu):
+  """dg_plan_refine == split_interval (Main_finite_difference.py:336-341) bit-exactly, and
+  the refined plan computes exactly what a plan created on the split mesh computes."""
+  import torch
+  rng = np.random.default_rng(13)
+  K0 = 300
+  S, mesh, op = setup(pkg, 4, K0, flux="burgers", limiter=True)
+  op.reserve(K0 + 8)
+  v_host = mesh.v_x.copy()
+  hs = torch.zeros(1, dtype=torch.float64, device=gpu)
+  for j in (0, 17, K0 - 1, 150, 151, 3):
+    idx = torch.tensor([j], dtype=torch.int64, device=gpu)
+    h_expect = v_host[j + 1] - v_host[j]
+    op.refine(idx, hs)
+    v_host = pkg.split_interval(v_host, j)
+    np.testing.assert_array_equal(op.v_x(), v_host)
+    assert float(hs.item()) == h_expect
+  assert op.K == K0 + 6 and not op.uniform
+  with pytest.raises(pkg._lib.DGLibraryError):
+    for _ in range(3):
+      op.refine(torch.tensor([0], dtype=torch.int64, device=gpu))
+  # same results as a fresh plan on the refined mesh
+  fresh = pkg.operators.DGAdvection1D(pkg.BaseGalerkin1D(n=4, v_x=op.v_x()), flux="burgers",
+                                      limiter=True)
+  S2 = setup1d.startup1d(4, fresh.mesh.v_x, metric="element")
+  u0 = dev(setup1d.to_elem_major(ic(S2, rng)), gpu)
+  dt = oadv.bench_dt(S2)
+  a_, b_ = u0.clone(), u0.clone()
+  op.forward(a_, 0.0, dt, 3)
+  fresh.forward(b_, 0.0, dt, 3)
+  np.testing.assert_array_equal(host(a_), host(b_))
+
+
+def test_refine_loop_with_device_argmax(pkg, gpu):
+  """Adapt loop on the device: init IC, limited fwd + adj, argmax |eta|, refine — the
+  refine indices agree with the oracle's argmax on the same snapshots whenever its top-2
+  gap exceeds the parity tolerance."""
+  import torch
+  N, K0, nsteps = 3, 120, 4
+  S, mesh, op = setup(pkg, N, K0, flux="burgers", limiter=True)
+  op.reserve(K0 + 5)
+  for _ in range(4):
+    v_x = op.v_x()
+    S = setup1d.startup1d(N, v_x, metric="element")
+    dt = oadv.bench_dt(S)
+    snaps = op.new_field(nsteps + 1)
+    op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
+    np.testing.assert_allclose(setup1d.from_elem_major(host(snaps[0]), N + 1),
+                               np.sin(2 * np.pi * S["x"]), atol=1e-13)
+    op.forward(snaps[0], 0.0, dt, nsteps, snaps)
+    w = snaps[nsteps].clone()
+    eta = torch.zeros(op.K, dtype=torch.float64, device=gpu)
+    op.adjoint(w, snaps, 0.0, dt, nsteps, eta=eta)
+    idx = op.argmax_async(eta, use_abs=True)
+    gs = [setup1d.from_elem_major(host(snaps[n]), N + 1) for n in range(nsteps + 1)]
+    times = [0.0]
+    for _n in range(nsteps):
+      times.append(times[-1] + dt)
+    _, eta_ref, _ = ob.adjoint_sweep(gs[-1], gs, times, dt, A, S, limit=True)
+    assert rel_err(host(eta), eta_ref) <= RTOL
+    top = np.sort(np.abs(eta_ref))[::-1]
+    j = int(idx.item())
+    if top[0] - top[1] > 1e-8 * top[0]:
+      assert j == int(np.argmax(np.abs(eta_ref)))
+    k_before = op.K
+    op.refine(idx)
+    assert op.K == k_before + 1
+    np.testing.assert_array_equal(op.v_x(), pkg.split_interval(v_x, j))
+
+
+@pytest.mark.slow
+def test_full_size_config3(pkg, gpu):
+  """BASELINE config 3 size (N=4, K=4,194,304, Burgers + limiter): 2 limited steps vs
+  the oracle, and the size-independent gradient identity of one adjoint step (central
+  difference of <g, S(u)>).  The directions are smooth: a random perturbation of size h
+  would itself trip SlopeLimitN's 1e-8 troubled-cell test in every cell."""
+  import torch
+  N, K, nsteps = 4, 1 << 22, 2
+  S, mesh, op = setup(pkg, N, K, flux="burgers", limiter=True)
+  x = S["x"]
+  u0 = np.sin(2 * np.pi * x) + 0.5 * (x > 0.5)
+  dt = oadv.bench_dt(S)
+  ref, _ = ob.forward_sweep(u0, 0.0, dt, nsteps, A, S)
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  snaps = op.new_field(nsteps + 1)
+  op.forward(u, 0.0, dt, nsteps, snaps)
+  assert rel_err(setup1d.from_elem_major(host(u), N + 1), ref[-1]) <= RTOL
+  del ref
+  g = dev(setup1d.to_elem_major(np.sin(5 * np.pi * x)), gpu)
+  d = dev(setup1d.to_elem_major(np.cos(3 * np.pi * x) + 0.3 * np.sin(7 * np.pi * x)), gpu)
+  w = g.clone()
+  op.adjoint(w, snaps[:2].contiguous(), 0.0, dt, 1)
+  # <g, S(u + h d) - S(u - h d)> / 2h, differencing the fields before the dot product: a
+  # difference of two 2e7-term dot products would carry their rounding (~1e-9) / 2h.
+  h = 1e-6
+  yp, ym = snaps[0] + h * d, snaps[0] - h * d
+  op.forward(yp, 0.0, dt, 1)
+  op.forward(ym, 0.0, dt, 1)
+  fd = float(torch.dot(g, yp - ym)) / (2 * h)
+  ad = float(torch.dot(w, d))
+  assert abs(fd - ad) <= 1e-5 * abs(ad)
