@@ -11,6 +11,9 @@ rank j > 0 runs IC j of the synthetic ensemble.  N GPUs = an ensem
 trajectories, one per GPU (weak scaling; the only exchange is the indicator all-gather).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--nsteps S] [--no-cpu-baseline]
+  python bench.py --config 3     BASELINE config 3: Burgers-type flux + SlopeLimitN after
+                                 every stage, K = 4,194,304, one refine iteration per step
+                                 (fwd + adj + argmax + device split; replicas per GPU)
 """
 import argparse
 import json
@@ -34,7 +37,9 @@ def parse():
   p.add_argument("--steps", type=int, default=10)
   p.add_argument("--warmup", type=int, default=3)
   p.add_argument("--N", type=int, default=4)
-  p.add_argument("--K", type=int, default=1 << 20)
+  p.add_argument("--config", type=int, default=2, choices=(2, 3),
+                 help="2: linear advection (headline); 3: Burgers flux + limiter refine loop")
+  p.add_argument("--K", type=int, default=None, help="elements (default 2^20; config 3: 2^22)")
   p.add_argument("--nsteps", type=int, default=20, help="time steps per sweep (each direction)")
   p.add_argument("--ics", type=int, default=0,
                  help="ensemble size over all ranks (config 4: --K 65536 --ics 1024); "
@@ -69,6 +74,122 @@ def cpu_baseline(N, K, nsteps):
                     f"K={K}, numpy oracle, 1 thread, {el:.1f} s"}
 
 
+def cpu_baseline_config3(N, K, nsteps):
+  """The oracle's limited Burgers forward step (numpy, one thread) on a bounded sample of
+  the config-3 workload.  Forward only: the oracle's adjoint is a coloured-Jacobian checker
+  (~100 tangent sweeps per step), not a CPU port worth timing, so this baseline flatters
+  the CPU by counting its forward rate for both directions."""
+  from threadpoolctl import threadpool_limits
+
+  from oracle import advec as oadv
+  from oracle import burgers as ob
+  from oracle import setup1d
+  S = setup1d.uniform_setup(N, K, metric="element")
+  a = 2 * np.pi
+  dt = oadv.bench_dt(S)
+  u0 = np.sin(2 * np.pi * S["x"])
+  with threadpool_limits(1):
+    t0 = time.perf_counter()
+    ob.forward_sweep(u0, 0.0, dt, nsteps, a, S)
+    el = time.perf_counter() - t0
+  dofs = (N + 1) * K * nsteps
+  return {"value": dofs / el, "unit": "DOF-updates/s", "cores": 1, "kind": "port",
+          "sample": f"{nsteps} forward LSERK4 steps with SlopeLimitN per stage (Burgers flux) "
+                    f"at N={N}, K={K}, numpy oracle, 1 thread, {el:.1f} s; forward rate "
+                    f"stands for both directions"}
+
+
+def main_config3(args, world, rank, dev):
+  """Config 3: one refine iteration per bench step on a trajectory of K elements (each
+  rank an independent replica; no data-path collective)."""
+  import importlib
+
+  import torch
+  import torch.distributed as dist
+  pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
+  N, K, nsteps = args.N, args.K or (1 << 22), args.nsteps
+  mesh = pkg.BaseGalerkin1D(n=N, k=K, domain=[0.0, 1.0])
+  run = pkg.adaptive.AdaptiveSweep(mesh, nsteps, args.warmup + args.steps + 1,
+                                   flux="burgers", limiter=True)
+  stream = torch.cuda.current_stream(dev)
+  for _ in range(args.warmup):
+    run.iterate()
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+  total = 0
+  t0 = time.perf_counter()
+  for s in range(args.steps):
+    dt = run.dt
+    evs[s][0].record(stream)
+    run.forward(dt)
+    evs[s][1].record(stream)
+    evs[s][2].record(stream)
+    run.adjoint(dt)
+    evs[s][3].record(stream)
+    total += run.refine()
+    ref_idx = run.sync()
+  torch.cuda.synchronize()
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize()
+  elapsed = time.perf_counter() - t0
+  if world > 1:
+    t = torch.tensor([elapsed, float(total)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
+    dist.all_reduce(t[1:2])
+    elapsed, total = float(t[0].item()), float(t[1].item())
+  Np = N + 1
+  k_mid = K + args.warmup + args.steps // 2
+  ms = run.op.steps_per_launch if run.op.steps_per_launch <= 2 else 2
+  fwd_launches = (nsteps + ms - 1) // ms
+  fwd_us = float(np.mean([e[0].elapsed_time(e[1]) for e in evs])) * 1e3 / fwd_launches
+  adj_us = float(np.mean([e[2].elapsed_time(e[3]) for e in evs])) * 1e3 / nsteps
+  # Algorithmic bytes per launch: forward reads u^n once and writes ms snapshots; the
+  # adjoint (one step per launch) reads w^{n+1} and u^n, writes w^n, updates eta.
+  fwd_bytes = (8.0 + 8.0 * ms) * Np * k_mid
+  adj_bytes = 24.0 * Np * k_mid + 16.0 * k_mid
+  out = {
+      "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
+      "value": total / elapsed,
+      "unit": "DOF-updates/s",
+      "n_gpus": world,
+      "steps": args.steps,
+      "warmup": args.warmup,
+      "ms_per_step": elapsed / args.steps * 1e3,
+      "higher_is_better": True,
+      "scaling": "weak",
+      "vs_baseline": None,
+      "dtype": "f64",
+      "data": "synthetic (u0 = sin(2 pi x), re-initialised on the refined mesh every step)",
+      "config": {"workload": (f"config 3: Burgers-type flux + SlopeLimitN after every LSERK4 "
+                              f"stage, N={N}, K={K}+refinements, {nsteps}+{nsteps} steps/sweep "
+                              f"+ DWR indicator + argmax + device element split per step"),
+                 "N": N, "K": K, "nsteps_per_sweep": nsteps, "parallelism": f"replicas{world}"},
+      "roofline": {"bound": "hbm", "achieved": adj_bytes / (adj_us * 1e-6) / 1e9,
+                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": adj_bytes / (adj_us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                   "kernel": f"k_adj_nl<{Np},burgers,limiter,nonuniform> (1 reverse step + "
+                             f"stage recompute + DWR per launch)",
+                   "launch_us": adj_us, "algorithmic_bytes": adj_bytes},
+      "roofline_fwd": {"bound": "hbm", "achieved": fwd_bytes / (fwd_us * 1e-6) / 1e9,
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": fwd_bytes / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                       "kernel": f"k_step_nl<{Np},burgers,limiter,nonuniform,{ms}>",
+                       "launch_us": fwd_us, "algorithmic_bytes": fwd_bytes},
+      "refine_index": ref_idx,
+      "K_final": run.K,
+  }
+  if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    out["cpu_baseline"] = cpu_baseline_config3(N, K, 2)
+  if rank == 0:
+    print(json.dumps(out), flush=True)
+  if world > 1:
+    dist.destroy_process_group()
+
+
 def main():
   args = parse()
   import torch
@@ -85,8 +206,10 @@ def main():
   if world > 1:
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
   dev = torch.device("cuda", local)
+  if args.config == 3:
+    return main_config3(args, world, rank, dev)
 
-  N, K, nsteps = args.N, args.K, args.nsteps
+  N, K, nsteps = args.N, args.K or (1 << 20), args.nsteps
   mesh = pkg.BaseGalerkin1D(n=N, k=K, domain=[0.0, 1.0])
   dt = mesh.cfl_dt()
   if args.ics > 0:  # config 4: the ensemble is sharded over the ranks (strong scaling)

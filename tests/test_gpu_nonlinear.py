@@ -290,3 +290,29 @@ def test_full_size_config3(pkg, gpu):
   fd = float(torch.dot(g, yp - ym)) / (2 * h)
   ad = float(torch.dot(w, d))
   assert abs(fd - ad) <= 1e-5 * abs(ad)
+
+
+def test_adaptive_sweep_driver(pkg, gpu):
+  """adaptive.AdaptiveSweep (the config-3 bench loop): its step size follows the CFL rule
+  on the refined mesh and its refine sequence equals the host-split loop's."""
+  import torch
+  N, K0, nsteps = 4, 200, 3
+  mesh = pkg.BaseGalerkin1D(n=N, k=K0)
+  run = pkg.adaptive.AdaptiveSweep(mesh, nsteps, 6)
+  v_x = mesh.v_x.copy()
+  for _ in range(5):
+    ref_mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+    assert abs(run.dt - ref_mesh.cfl_dt()) <= 1e-12 * ref_mesh.cfl_dt()
+    dt = run.dt
+    _, j = run.iterate()
+    # host-side replay of the same iteration on a fresh plan
+    op = pkg.operators.DGAdvection1D(ref_mesh, flux="burgers", limiter=True)
+    snaps = op.new_field(nsteps + 1)
+    op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
+    op.forward(snaps[0], 0.0, dt, nsteps, snaps)
+    eta = torch.zeros(op.K, dtype=torch.float64, device=gpu)
+    op.adjoint(snaps[nsteps], snaps, 0.0, dt, nsteps, eta=eta)
+    assert j == op.argmax(eta, use_abs=True)
+    v_x = pkg.split_interval(v_x, j)
+    np.testing.assert_array_equal(run.op.v_x(), v_x)
+  assert run.K == K0 + 5
