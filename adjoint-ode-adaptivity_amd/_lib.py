@@ -16,6 +16,7 @@ DG_OK, DG_ERR_ARG, DG_ERR_HIP, DG_ERR_NOMEM = 0, -1, -2, -3
 DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T = 0, 1
 DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
 DG_TUNE_TILE_WIDTH, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
+DG_TUNE_LANE_ELEMENTS = 4
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE = 0, 1
 

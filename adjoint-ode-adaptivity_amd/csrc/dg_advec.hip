@@ -31,28 +31,6 @@ int fail(int code, const std::string& msg) {
 namespace {
 using namespace dgk;
 
-// Arguments of a launch that advances MS time steps of NS stages each.
-template <int NP, int NS, int MS> struct StepArgs {
-  EOArgs<NP> op;
-  double sc;            // dt (non-uniform meshes multiply by scale[k]; uniform: folded in op)
-  double uin[MS * NS];  // inflow value at each stage time
-  int64_t ktot;         // batch * K elements
-  int64_t stride;       // doubles between consecutive snapshots
-  int32_t K;            // elements per trajectory
-  int32_t xcd;          // XCD-aware tile order (speed only)
-};
-
-template <int NP, int MS> struct AdjArgs {
-  EOArgs<NP> op;
-  double sc;
-  double uin_res[MS];  // inflow value at t_{n+st+1} for the residual of step st
-  double src[MS];      // functional source coefficient for node n+st+1
-  int64_t ktot;
-  int64_t stride;      // doubles between consecutive snapshots
-  int32_t K;
-  int32_t has_eta;
-  int32_t xcd;         // XCD-aware tile order (speed only)
-};
 
 // ---------------------------------------------------------------------------
 // Forward fused kernel: MS time steps of NS stages (AdvecRHS1D + the low-storage update)
@@ -158,9 +136,10 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
         // trajectory reads the inflow value, the last one its own right face (du1 = 0).
         const int iL = EDGE && E[m].first ? CB + st * NS + s : fR + el;
         const int iR = EDGE && E[m].last ? fR + el + 1 : fL + el + 2;
-        const double du0 = u0[m] - lds[iL];
-        const double du1 = uN[m] - lds[iR];
-        const double dlt = du0 - du1, sig = du0 + du1;
+        // The own faces' lift parts sit in the folded volume blocks (make_eo, fold):
+        // only uR - uL and uL + uR remain.
+        const double uL = lds[iL], uR = lds[iR];
+        const double dlt = uR - uL, sig = -(uL + uR);
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
           if constexpr (UNI) {  // r = A_s r + dt*L u, dt*2/h folded into the operator
@@ -355,10 +334,11 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
           qo[m][k] = UNI ? lo_[m][k] : sc[m] * lo_[m][k];
           gs = fma(args.op.lo[k], qo[m][k], gs);
         }
-        // adjoints of du0 and du1 (du0 - du1 feeds the even part, du0 + du1 the odd part)
+        // adjoints of the left / right neighbour face values uL, uR (folded operator:
+        // dlt = uR - uL feeds the even part, sig = -(uL + uR) the odd part):
+        // d/duL = -(gd + gs) = -g0, d/duR = gd - gs = -g1
         g0[m] = gd + gs;
         g1[m] = gs - gd;
-        if constexpr (EDGE) g1[m] = E[m].last ? 0.0 : g1[m];
         lds[f0 + el + 1] = g0[m];
         lds[f1 + el + 1] = g1[m];
         __builtin_amdgcn_sched_barrier(0);  // face writes first
@@ -391,13 +371,15 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 #pragma unroll
       for (int m = 0; m < EPL; ++m) {
         const int el = m * LB + lane;
-        // du0 = u_0 - (left neighbour's u_N); du1 = u_N - (right neighbour's u_0), with
-        // u_0 = e_0 + o_0 and u_N = e_0 - o_0.
-        // g1 of element k-1 and g0 of element k+1 (edge tiles: zero across trajectory ends)
+        // This element's u_0 = e_0 + o_0 is the right neighbour value uR of element k-1
+        // (adjoint -g1 there), its u_N = e_0 - o_0 the left value uL of element k+1
+        // (adjoint -g0 there).  Edge tiles: a trajectory's first element has uL = inflow
+        // (nothing arrives from the left); its last one has uR = its own u_N (du1 = 0), so
+        // its own -g1 lands on its u_N.
         const double gl = lds[EDGE && E[m].first ? CB + MS : f1 + el];
-        const double gr = lds[EDGE && E[m].last ? CB + MS : f0 + el + 2];
-        we[m][0] += (g0[m] + g1[m]) - (gr + gl);
-        wo[m][0] += (g0[m] - g1[m]) + (gr - gl);
+        const double gr = lds[EDGE && E[m].last ? f1 + el + 1 : f0 + el + 2];
+        we[m][0] -= gl + gr;
+        wo[m][0] += gr - gl;
       }
     }
   }
@@ -734,7 +716,7 @@ template <int NP, int NS, int W, int MS>
 int launch_step_e(const dg_plan* p, const double* in, double* snap, double* last,
                   const double* times, double dt, hipStream_t st) {
   StepArgs<NP, NS, MS> a;
-  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
   a.sc = dt;  // non-uniform meshes multiply by scale[k] in the kernel
   for (int m = 0; m < MS; ++m)
     for (int s = 0; s < NS; ++s) a.uin[m * NS + s] = inflow_value(p, times[m] + RK<NS>::C(s) * dt);
@@ -759,7 +741,7 @@ int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double
                  double* eta, const double* t_next, const double* src, double dt,
                  hipStream_t st) {
   AdjArgs<NP, MS> a;
-  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
   a.sc = dt;
   for (int m = 0; m < MS; ++m) {
     a.uin_res[m] = inflow_value(p, t_next[m]);
@@ -783,13 +765,15 @@ int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double
 }
 
 // Instantiated shapes: tile width W in {1, 2} (256 or 512 elements per tile) x steps per
-// launch in {1, 2, 4}; 4 steps per launch only for Np <= 8 (at Np = 9 hipcc/ROCm 7.2 fails
-// instruction selection for that shape; chunk() never asks for it there).
+// launch in {1, 2, 4}, plus 8 steps per launch on 512-element tiles; 4 and 8 steps per
+// launch only for Np <= 8 (at Np = 9 hipcc/ROCm 7.2 fails instruction selection for the
+// 4-step shape; effective_msteps() never asks for them there).
 template <int NP, int NS>
 int launch_step_t(const dg_plan* p, int ms, const double* in, double* snap, double* last,
                   const double* times, double dt, hipStream_t st) {
   const bool w2 = p->tile_width == 2;
   if constexpr (NP <= 8) {
+    if (ms == 8) return launch_step_e<NP, NS, 2, 8>(p, in, snap, last, times, dt, st);
     if (ms == 4 && w2) return launch_step_e<NP, NS, 2, 4>(p, in, snap, last, times, dt, st);
     if (ms == 4) return launch_step_e<NP, NS, 1, 4>(p, in, snap, last, times, dt, st);
   }
@@ -805,6 +789,8 @@ int launch_adj_t(const dg_plan* p, int ms, const double* win, double* wout, cons
                  hipStream_t st) {
   const bool w2 = p->tile_width == 2;
   if constexpr (NP <= 8) {
+    if (ms == 8)
+      return launch_adj_e<NP, NS, 2, 8>(p, win, wout, snap, eta, t_next, src, dt, st);
     if (ms == 4 && w2)
       return launch_adj_e<NP, NS, 2, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
     if (ms == 4) return launch_adj_e<NP, NS, 1, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
@@ -819,6 +805,8 @@ int launch_adj_t(const dg_plan* p, int ms, const double* win, double* wout, cons
 int launch_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
                 const double* times, double dt, hipStream_t st) {
   int rc = DG_OK;
+  if (p->lane_elems != 0 && p->nstages == 5 && p->NP <= 8)
+    return wave_launch_step(p, ms, in, snap, last, times, dt, st);
   if (p->nstages == 5) {
     DG_DISPATCH_NP(p->NP, rc = (launch_step_t<NP, 5>(p, ms, in, snap, last, times, dt, st)));
   } else {
@@ -840,14 +828,23 @@ int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const 
   return rc;
 }
 
+// Steps per launch the plan's shape allows: 8 only with 512-element tiles (the cone is
+// 8*NS elements per side) and Np <= 8; at Np = 9 at most 2 (hipcc/ROCm 7.2 fails
+// instruction selection for the 4-step shape there).
+inline int effective_msteps(const dg_plan* p) {
+  int m = p->msteps;
+  if (m == 8 && !(p->tile_width == 2 || p->lane_elems == 8)) m = 4;
+  if (p->NP > 8 && m > 2) m = 2;
+  return m;
+}
+
 // Steps per launch for the next chunk of `left` steps (greedy over {4, 2, 1}, capped by
 // the plan's setting).
 inline int chunk(const dg_plan* p, int left) {
-  int m = (p->NP > 8 && p->msteps > 2) ? 2 : p->msteps;
+  int m = effective_msteps(p);
   while (m > left) m >>= 1;
   return m < 1 ? 1 : m;
 }
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -917,14 +914,21 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   p->uniform = (hmax - hmin) <= 1e-12 * hmean;
   p->s_uniform = 2.0 / hmean;
 
+  // Per-N default shape (config 5 sweep, profiles/r01/tune/N*.json): 512-element tiles
+  // pay off at low order, where a lane's work per stage is small.
+  p->tile_width = (N <= 2) ? 2 : 1;
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);
       if (k == 1 || k == 2) p->tile_width = k;
     }
+    if (const char* v = std::getenv("DG_LANE_ELEMENTS")) {
+      const int k = std::atoi(v);
+      if (k == 0 || k == 2 || k == 4 || k == 8) p->lane_elems = k;
+    }
     if (const char* v = std::getenv("DG_STEPS_PER_LAUNCH")) {
       const int k = std::atoi(v);
-      if (k == 1 || k == 2 || k == 4) p->msteps = k;
+      if (k == 1 || k == 2 || k == 4 || k == 8) p->msteps = k;
     }
   }
   auto cleanup = [&](const std::string& m) {
@@ -969,7 +973,7 @@ int dg_plan_query(const dg_plan* p, int64_t out[8]) {
   out[4] = p->uniform ? 1 : 0;
   out[5] = p->nstages;
   out[6] = p->tile_width;
-  out[7] = (p->NP > 8 && p->msteps > 2) ? 2 : p->msteps;
+  out[7] = effective_msteps(p);
   return DG_OK;
 }
 
@@ -983,9 +987,14 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
     case DG_TUNE_XCD_ORDER:
       p->xcd_order = value ? 1 : 0;
       return DG_OK;
+    case DG_TUNE_LANE_ELEMENTS:
+      if (value != 0 && value != 2 && value != 4 && value != 8)
+        return fail(DG_ERR_ARG, "lane elements must be 0, 2, 4 or 8");
+      p->lane_elems = int(value);
+      return DG_OK;
     case DG_TUNE_STEPS_PER_LAUNCH:
-      if (value != 1 && value != 2 && value != 4)
-        return fail(DG_ERR_ARG, "steps per launch must be 1, 2 or 4");
+      if (value != 1 && value != 2 && value != 4 && value != 8)
+        return fail(DG_ERR_ARG, "steps per launch must be 1, 2, 4 or 8");
       p->msteps = int(value);
       return DG_OK;
     default:

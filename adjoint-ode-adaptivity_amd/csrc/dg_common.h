@@ -91,6 +91,29 @@ template <int NP> struct EOArgs {
   double lo[NO];
 };
 
+// Arguments of a launch that advances MS time steps of NS stages each.
+template <int NP, int NS, int MS> struct StepArgs {
+  EOArgs<NP> op;
+  double sc;            // dt (non-uniform meshes multiply by scale[k]; uniform: folded in op)
+  double uin[MS * NS];  // inflow value at each stage time
+  int64_t ktot;         // batch * K elements
+  int64_t stride;       // doubles between consecutive snapshots
+  int32_t K;            // elements per trajectory
+  int32_t xcd;          // XCD-aware tile order (speed only)
+};
+
+template <int NP, int MS> struct AdjArgs {
+  EOArgs<NP> op;
+  double sc;
+  double uin_res[MS];  // inflow value at t_{n+st+1} for the residual of step st
+  double src[MS];      // functional source coefficient for node n+st+1
+  int64_t ktot;
+  int64_t stride;      // doubles between consecutive snapshots
+  int32_t K;
+  int32_t has_eta;
+  int32_t xcd;         // XCD-aware tile order (speed only)
+};
+
 // ---------------------------------------------------------------------------
 // Tile staging helpers.  A tile is the contiguous range of doubles of kBlock
 // consecutive elements starting at element e0 (which may be negative or run past
@@ -339,9 +362,10 @@ struct dg_plan {
   double* d_pv = nullptr;
   int64_t* d_pi = nullptr;
   // tuning (dg_plan_tune): tile width of the step kernels (tile = 256*tile_width elements)
-  int tile_width = 1;
+  int tile_width = 1;  // dg_plan_create: 2 for N <= 2 (measured per-N)
   int msteps = 4;  // time steps fused per launch (1, 2 or 4)
   int xcd_order = 1;  // XCD-aware tile order
+  int lane_elems = 0;  // 0: workgroup tiles (one element per lane); 2 or 4: wave tiles
   // physics (dg_plan_set_physics): DG_FLUX_LINEAR / DG_FLUX_BURGERS, SlopeLimitN per stage
   int flux = 0;
   int limiter = 0;
@@ -367,7 +391,12 @@ template <int NP> OpArgs<NP> make_op(const dg_plan* p, double scale = 1.0) {
 
 // Even/odd blocks of the element operator (see EOArgs).  Returns false if the operator
 // is not centro-(anti)symmetric to 1e-12, i.e. the nodes are not symmetric.
-template <int NP> bool make_eo(const dg_plan* p, double scale, EOArgs<NP>* out) {
+// fold = true: the own-face parts of the lift term go into the volume blocks.  With
+// du0 = u_0 - uL, du1 = u_N - uR and u_0 - u_N = 2 o_0, u_0 + u_N = 2 e_0:
+//   le*(du0 - du1) = 2 le o_0 + le*(uR - uL),   lo*(du0 + du1) = 2 lo e_0 - lo*(uL + uR)
+// so Qeo(:,0) += 2 le and Qoe(:,0) += 2 lo, and a stage needs only the neighbours' faces
+// (uR - uL, uL + uR): two fp64 ops fewer per stage forward, four in the adjoint.
+template <int NP> bool make_eo(const dg_plan* p, double scale, EOArgs<NP>* out, bool fold = false) {
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   double Dm[NP][NP], L0[NP], L1[NP], T[NP][NP] = {}, Ti[NP][NP] = {};
   for (int i = 0; i < NP; ++i) {
@@ -421,6 +450,10 @@ template <int NP> bool make_eo(const dg_plan* p, double scale, EOArgs<NP>* out) 
       for (int j = 0; j < NE; ++j) out->Qoe[k * NE + j] = Q[NE + k][j];
     for (int k = 0; k < NE; ++k) out->le[k] = 0.5 * (l0[k] - l1[k]);
     for (int k = 0; k < NO; ++k) out->lo[k] = 0.5 * (l0[NE + k] + l1[NE + k]);
+    if (fold) {
+      for (int k = 0; k < NE; ++k) out->Qeo[k * NO] += 2.0 * out->le[k];
+      for (int k = 0; k < NO; ++k) out->Qoe[k * NE] += 2.0 * out->lo[k];
+    }
   }
   return ok;
 }
@@ -448,5 +481,10 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
            hipStream_t st);
 int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,
            double src_coef, double* eta, hipStream_t st);
+
+// Wave-tile variants of the linear LSERK4 step kernels (dg_wave.hip), selected by
+// plan->lane_elems; `times` as for the workgroup-tile launchers.
+int wave_launch_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
+                     const double* times, double dt, hipStream_t st);
 
 }  // namespace dgk

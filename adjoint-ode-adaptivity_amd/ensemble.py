@@ -102,6 +102,8 @@ class EnsembleSweep:
     self._graphs[1].replay()
 
   def reduce(self):
+    if self.batch == 1:  # one IC: the partial sum is eta itself
+      return self.eta
     sum_rows(self.eta, self.batch, out=self.partial)
     return self.partial
 
@@ -138,6 +140,7 @@ def gather_indicator(partial, n_total, reducer, group=None):
     stacked = torch.stack(bufs)
   else:
     stacked = partial.reshape(1, -1)
-  total = reducer.sum_rows(stacked)
-  mean = total / float(n_total)
+  # one slice: its sum is itself; dividing by 1 is exact (both shortcuts are bit-identical)
+  total = reducer.sum_rows(stacked) if stacked.shape[0] > 1 else partial
+  mean = total / float(n_total) if n_total != 1 else total
   return mean, reducer.argmax(mean)

@@ -118,15 +118,19 @@ class DGAdvection1D:
   def __exit__(self, *exc):
     self.close()
 
-  def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None):
+  def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
-    element per lane), ``steps_per_launch`` (1, 2 or 4) time steps fused per launch, and
+    element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
+    fused per launch, and
     ``xcd_order`` gives each XCD a contiguous range of tiles.  Tile width and order do not
     change the arithmetic; steps per launch changes it at rounding level (the state stays
     in even/odd coordinates between fused steps)."""
     if xcd_order is not None:
       _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_XCD_ORDER, int(xcd_order)),
                  "dg_plan_tune")
+    if lane_elements is not None:  # forward steps on one-wave tiles (0 = workgroup tiles)
+      _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_LANE_ELEMENTS,
+                                        int(lane_elements)), "dg_plan_tune")
     if tile_width is not None:
       _lib.check(self._lib.dg_plan_tune(self._plan, _lib.DG_TUNE_TILE_WIDTH,
                                         int(tile_width)), "dg_plan_tune")

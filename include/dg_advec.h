@@ -80,12 +80,18 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  * bit-identical; steps per launch changes it at rounding level only.
  *   DG_TUNE_TILE_WIDTH        1 or 2: workgroups of 256*value lanes, one element per lane,
  *                             own tiles of 256*value elements (2: half the halo overhead)
- *   DG_TUNE_STEPS_PER_LAUNCH  time steps fused per launch: 1, 2 or 4 (temporal blocking:
+ *   DG_TUNE_STEPS_PER_LAUNCH  time steps fused per launch: 1, 2, 4 or 8 (temporal blocking:
  *                             each launch reads its input state once and writes every
- *                             intermediate snapshot; halo = steps*stages elements per side)
+ *                             intermediate snapshot; halo = steps*stages elements per side;
+ *                             8 needs tile width 2, else 4 is used; Np = 9 caps it at 2)
  *   DG_TUNE_XCD_ORDER         0/1: give each XCD a contiguous range of tiles (speed only)
- * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH. */
-enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3 };
+ *   DG_TUNE_LANE_ELEMENTS     0: workgroup tiles, one element per lane; 2 or 4: forward steps
+ *                             on one-wave tiles of 64*value elements, value consecutive
+ *                             elements per lane, cross-lane faces by DPP (LSERK4, Np <= 8;
+ *                             bit-identical to the workgroup tiles at equal steps per launch)
+ * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS. */
+enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
+       DG_TUNE_LANE_ELEMENTS = 4 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* Physics of the plan's steppers.  Default: DG_FLUX_LINEAR + DG_LIMIT_NONE (AdvecRHS1D).

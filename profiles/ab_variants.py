@@ -38,7 +38,8 @@ def main():
   st = torch.cuda.current_stream()
   for r in range(a.rounds + 1):
     for v in variants:
-      op.tune(tile_width=v[0], steps_per_launch=v[1], xcd_order=(v[2] if len(v) > 2 else 1))
+      op.tune(tile_width=v[0], steps_per_launch=v[1], xcd_order=(v[2] if len(v) > 2 else 1),
+              lane_elements=(v[3] if len(v) > 3 else 0))
       e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
       e[0].record(st)
       op.forward(snaps[0], 0.0, dt, a.nsteps, snaps)
@@ -61,7 +62,8 @@ def main():
   out = {}
   for v in variants:
     f, d = float(np.median(res[v]["fwd"])), float(np.median(res[v]["adj"]))
-    out[f"width={v[0]} steps/launch={v[1]} xcd={v[2] if len(v) > 2 else 1}"] = {"fwd_us": f, "fwd_GBs": fb / f / 1e3, "adj_us": d,
+    out[f"width={v[0]} steps/launch={v[1]} xcd={v[2] if len(v) > 2 else 1} "
+        f"lane_elems={v[3] if len(v) > 3 else 0}"] = {"fwd_us": f, "fwd_GBs": fb / f / 1e3, "adj_us": d,
                                          "adj_GBs": ab / d / 1e3,
                                          "fwd_nosnap_us": float(np.median(res[v]["fwd_nosnap"])),
                                          "fwd_min_us": float(np.min(res[v]["fwd"])),

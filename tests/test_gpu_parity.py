@@ -336,9 +336,13 @@ def test_kernel_variants_bit_identical(pkg, gpu, N, K):
   dt = oadv.bench_dt(S)
   outs = []
   nsteps = 7  # exercises the greedy 4 + 2 + 1 chunking
-  shapes = ((1, 1, 1), (2, 1, 0), (1, 2, 1), (1, 4, 1), (2, 4, 0), (1, 4, 0), (2, 2, 1))
-  for width, ms, xcd in shapes:
-    op = make_op(pkg, mesh).tune(tile_width=width, steps_per_launch=ms, xcd_order=xcd)
+  shapes = ((1, 1, 1, 0), (2, 1, 0, 0), (1, 2, 1, 0), (1, 4, 1, 0), (2, 4, 0, 0), (1, 4, 0, 0),
+            (2, 2, 1, 0), (1, 4, 1, 4), (1, 4, 1, 2), (1, 2, 1, 4), (2, 8, 1, 0))
+  for width, ms, xcd, lanes in shapes:
+    if lanes and N == 8:
+      lanes = 0  # wave tiles cover Np <= 8
+    op = make_op(pkg, mesh).tune(tile_width=width, steps_per_launch=ms, xcd_order=xcd,
+                                 lane_elements=lanes)
     snaps = op.new_field(nsteps + 1)
     op.forward(u0.clone(), 0.0, dt, nsteps, snaps)
     w = snaps[nsteps].clone()
@@ -352,7 +356,8 @@ def test_kernel_variants_bit_identical(pkg, gpu, N, K):
   # step), so different steps-per-launch agree to rounding.
   for a_, b_ in zip(outs[0], outs[1]):
     np.testing.assert_array_equal(a_, b_)
-  for i, j in ((3, 4), (3, 5)):  # same steps per launch, other lane packing / tile order
+  # same steps per launch, other lane packing / tile order / wave tiles
+  for i, j in ((3, 4), (3, 5), (3, 7), (3, 8), (2, 9)):
     for a_, b_ in zip(outs[i], outs[j]):
       np.testing.assert_array_equal(a_, b_)
   # States agree to 1e-12; the indicator (a cancellation-limited jump residual) to RTOL.
