@@ -46,7 +46,9 @@ def parse():
                       "default: one trajectory per rank (config 2 per GPU, weak scaling)")
   p.add_argument("--no-cpu-baseline", action="store_true")
   p.add_argument("--cpu-steps", type=int, default=12, help="time steps of the CPU sample")
-  p.add_argument("--eager", action="store_true", help="launch the sweeps eagerly (no HIP graph)")
+  p.add_argument("--graph", action="store_true",
+                 help="replay each sweep as a captured HIP graph (measured 1-3%% slower than "
+                      "eager launches on this path, profiles/r01/bench_eager_vs_graph.txt)")
   return p.parse_args()
 
 
@@ -223,7 +225,7 @@ def main():
     n_total = world
   sweep = ens.EnsembleSweep(mesh, ics, nsteps, dt, params=params)
   reducer = ens.DeviceReducer(sweep.op)
-  if not args.eager:
+  if args.graph:
     sweep.capture()  # each sweep becomes one HIP graph launch
   stream = torch.cuda.current_stream(dev)
   idx_host = torch.zeros(1, dtype=torch.int64).pin_memory()
@@ -231,11 +233,11 @@ def main():
   def one_step(ev=None):
     if ev:
       ev[0].record(stream)
-    sweep.forward() if args.eager else sweep.forward_graph()
+    sweep.forward_graph() if args.graph else sweep.forward()
     if ev:
       ev[1].record(stream)
       ev[2].record(stream)
-    sweep.adjoint() if args.eager else sweep.adjoint_graph()
+    sweep.adjoint_graph() if args.graph else sweep.adjoint()
     if ev:
       ev[3].record(stream)
     partial = sweep.reduce()
