@@ -12,17 +12,18 @@ Submodules:
   factory    Problem / Funs / AdaptFuns / AdaptState / FunFactory adapt-loop API
   ensemble   ensembles of initial conditions sharded over ranks (RCCL all-gather)
   adaptive   device-resident spatial adapt loop (config 3: fwd + adj + refine)
+  dgtime     batched DG-in-time marches + DWR for ODE ensembles (matlab/MAIN.m loop)
   build_ext  in-tree hipcc build of lib/libdgadv.so
 """
 from . import _lib, galerkin  # noqa: F401
 from .galerkin import BaseGalerkin1D, split_interval  # noqa: F401
 
-__all__ = ["BaseGalerkin1D", "split_interval", "operators", "factory", "ensemble", "adaptive", "galerkin"]
+__all__ = ["BaseGalerkin1D", "split_interval", "operators", "factory", "ensemble", "adaptive", "dgtime", "galerkin"]
 
 
 def __getattr__(name):
   # torch-dependent modules load on first use (the host setup does not need torch).
-  if name in ("operators", "factory", "ensemble", "adaptive"):
+  if name in ("operators", "factory", "ensemble", "adaptive", "dgtime"):
     import importlib
     return importlib.import_module(f"{__name__}.{name}")
   if name == "DGAdvection1D":

@@ -46,6 +46,10 @@ SIGNATURES = {
     "dg_argmax": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "dg_sum_rows": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "dg_init_sine": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "dg_time_march": (_i32, [_i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp, ctypes.c_double,
+                             _i32, _vp, _vp, _vp]),
+    "dg_time_adjoint": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp,
+                               _vp, _vp, _vp, _vp]),
 }
 
 

@@ -175,6 +175,35 @@ int dg_sum_rows(const double* x, int64_t rows, int64_t n, double* out, void* str
 int dg_init_sine(const dg_plan* plan, const double* amp, const double* freq,
                  const double* phase, double* u, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * DG-in-time marches for ensembles of the scalar ODE du/dt = sin(u).
+ * Replaces matlab/dg_march.m (nonlinear branch, :36-77), matlab/adj_march.m (nonlinear
+ * branch, :61-119) and the fem_setup.m operators they rebuild per slab; one ensemble member
+ * (initial value y0[ic]) per lane, all members on the same slab mesh `times` (n_slabs+1
+ * host-computed device doubles).  Reference-element operators are computed on the host
+ * (adjoint-ode-adaptivity_amd/dgtime.py) and passed as device arrays, row-major.
+ * --------------------------------------------------------------------------------------- */
+
+/* Forward march, order Np-1, Newton per slab until ||U_old - U_next|| <= tol or maxit
+ * (dg_march.m:44-68).  S = (V V')\Dr [Np][Np]; Phi [nq][Np] nodal basis at the nq Gauss
+ * points (fem_setup.m:30-38); wq [nq] Gauss weights.  Y[(k*Np + i)*n_ics + ic] receives the
+ * nodal values of slab k; iters (nullable) [k*n_ics + ic] the Newton iteration counts. */
+int dg_time_march(int Np, int nq, const double* S, const double* Phi, const double* wq,
+                  int n_slabs, const double* times, int64_t n_ics, const double* y0, double tol,
+                  int maxit, double* Y, int32_t* iters, void* stream);
+
+/* Adjoint march (order Np_fwd) for J = integral of u and the dual-weighted residual
+ * err(k) = v_k' R_k(u_h) of the forward solution Y (order Np_fwd-1) (adj_march.m:66-117),
+ * with the reference's slab mapping hk = x(1) - x(end) (adj_march.m:73).  Sa = inv(V V')*Dr
+ * and Ma = inv(V V') [Na][Na] (Na = Np_fwd+1); Phia [nq][Na] adjoint basis at the Gauss
+ * points; Pext [nq][Np_fwd] forward basis at the points adj_march.m:79 evaluates;
+ * Ifa [Na][Np_fwd] forward basis at the adjoint nodes; wq [nq].  V[(k*Na + i)*n_ics + ic],
+ * err[ic*n_slabs + k]. */
+int dg_time_adjoint(int Np_fwd, int nq, const double* Sa, const double* Ma, const double* Phia,
+                    const double* Pext, const double* Ifa, const double* wq, int n_slabs,
+                    const double* times, int64_t n_ics, const double* y0, const double* Y,
+                    double* V, double* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
