@@ -83,14 +83,13 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
   }
-  __syncthreads();  // the face arrays below alias the staging image
 
   double re[EPL][NE], ro[EPL][NO];
 #pragma unroll
   for (int st = 0; st < MS; ++st) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const int fL = (s & 1) * 2 * (T + 2);  // faceL = lds[fL ...], faceR = lds[fR ...]
+      const int fL = G::kFB + (s & 1) * 2 * (T + 2);  // faceL = lds[fL ...], faceR = lds[fR ...]
       const int fR = fL + (T + 2);
       double u0[EPL], uN[EPL];
       double pe[EPL][NE], po[EPL][NO];
@@ -163,7 +162,8 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
       }
     }
     if (snap != nullptr || st == MS - 1) {
-      __syncthreads();  // the last stage's face reads are done before the image is rewritten
+      // The image's last readers (staging reads, the previous step's store) are at least
+      // one stage barrier behind; the faces live elsewhere.
       stage_out<NP, W, H>(lds, ev, od, false);
       __syncthreads();
       if constexpr (EDGE) {
@@ -173,7 +173,6 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
         if (snap != nullptr) store_full<TE * NP, LB>(snap + st * args.stride, o0, lds);
         if (st == MS - 1 && last != nullptr) store_full<TE * NP, LB>(last, o0, lds);
       }
-      if (st < MS - 1) __syncthreads();  // the next stage's faces alias the image
     }
   }
 }
@@ -261,7 +260,9 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 
 #pragma unroll
   for (int st = MS - 1; st >= 0; --st) {
-    __syncthreads();  // previous reads of the image (w tile or the last stage's faces) done
+    // The w tile's readers must be done before the first snapshot overwrites the image;
+    // later snapshots follow 5 stage barriers after the previous one's reads.
+    if (st == MS - 1) __syncthreads();
     tile_commit<NP, W>(pu, lds);
     const int off = pu.off;
     __syncthreads();
@@ -301,7 +302,6 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
         eacc[m] += c;
       }
     }
-    __syncthreads();  // the face arrays below alias the staging image
 
     double le_[EPL][NE], lo_[EPL][NO];  // the stage residual's adjoint
 #pragma unroll
@@ -314,7 +314,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 #pragma unroll
     for (int ss = 0; ss < NS; ++ss) {
       const int s = NS - 1 - ss;
-      const int f0 = (ss & 1) * 2 * (T + 2);  // g0 = lds[f0 ...], g1 = lds[f1 ...]
+      const int f0 = G::kFB + (ss & 1) * 2 * (T + 2);  // g0 = lds[f0 ...], g1 = lds[f1 ...]
       const int f1 = f0 + (T + 2);
       double qe[EPL][NE], qo[EPL][NO];
       double g0[EPL], g1[EPL];
@@ -387,8 +387,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 #pragma unroll
   for (int m = 0; m < EPL; ++m)
     if (args.has_eta && E[m].valid) eta[E[m].e] += eacc[m];
-  __syncthreads();  // the last stage's face reads are done before the image is rewritten
-  stage_out<NP, W, H>(lds, we, wo, true);
+  stage_out<NP, W, H>(lds, we, wo, true);  // the image's last reads are 5 barriers behind
   __syncthreads();
   const int64_t o0 = tile * TE * NP;
   if constexpr (EDGE) {
