@@ -50,6 +50,7 @@ SIGNATURES = {
                              _i32, _vp, _vp, _vp]),
     "dg_time_adjoint": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp,
                                _vp, _vp, _vp, _vp]),
+    "dg_fd_adapt_sweep": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp]),
 }
 
 

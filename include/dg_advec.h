@@ -204,6 +204,19 @@ int dg_time_adjoint(int Np_fwd, int nq, const double* Sa, const double* Ma, cons
                     const double* times, int64_t n_ics, const double* y0, const double* Y,
                     double* V, double* err, void* stream);
 
+/* Finite-difference DWR adapt sweep for ensembles of du/dt = sin(u), J = int u^2
+ * (python/Main_finite_difference.py:34-94 and :270-277), one member (initial
+ * value u0[ic]) per lane: forward Euler on the n_steps coarse steps dt_n, the discrete
+ * adjoint on the ref_factor-refined grid (the bidiagonal (J_F^T - I) v = -K of :73 as its
+ * backward recursion), the adjoint-weighted residual and its per-step window sums.
+ * t_coarse [n_steps+1] and t_fine [n_steps*ref_factor+1] are the cumulative times of
+ * interpU (:27-28); interp_code [n_steps*ref_factor+1] says where np.interp takes each fine
+ * value (j >= 0: interval j; -(j+1): node j exactly).  Outputs: U[n*n_ics + ic] (coarse
+ * solution), V (nullable) [n*n_ics + ic] (fine adjoint), err_steps[ic*n_steps + r]. */
+int dg_fd_adapt_sweep(int n_steps, int ref_factor, const double* dt_n, const double* t_coarse,
+                      const double* t_fine, const int32_t* interp_code, const double* u0,
+                      int64_t n_ics, double* U, double* V, double* err_steps, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
