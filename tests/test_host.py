@@ -145,3 +145,31 @@ def test_fd_ensemble_interp_codes_reproduce_np_interp(pkg):
         slope = (u[c + 1] - u[c]) / (tc[c + 1] - tc[c])
         got[i] = slope * (tf[i] - tc[c]) + u[c]
     np.testing.assert_array_equal(got, np.interp(tf, tc, u))
+
+
+def test_save_to_1d_global_data_roundtrip(pkg, tmp_path):
+  """Save_to_1D_global_data.m-compatible dumps: the One_code.mlx
+  configuration written and read back, checked against the MATLAB goldens."""
+  import importlib
+  gio = importlib.import_module("adjoint-ode-adaptivity_amd.globals_io")
+  with open(os.path.join(GOLDEN, "one_code_mlx_golden.json")) as f:
+    gold = json.load(f)
+  g = pkg.BaseGalerkin1D(n=2, k=20)
+  paths = gio.save_global_data(g, str(tmp_path))
+  assert len(paths) == len(gio.NAMES)
+  d = gio.load_global_data(str(tmp_path))
+  assert set(d) == set(gio.NAMES)
+  np.testing.assert_allclose(d["Dr"], g.d_r, rtol=1e-14)
+  np.testing.assert_allclose(d["x"], g.x, rtol=1e-14)
+  assert d["vmapM"].shape == (40, 1) and d["VX"].shape == (1, 21) and d["rk4a"].shape == (1, 5)
+  assert int(d["K"][0, 0]) == 20 and int(d["Np"][0, 0]) == 3 and int(d["mapO"][0, 0]) == 40
+  checked = set()
+  for e in gold["entries"]:  # the displayed MATLAB values (4 decimals, some truncated)
+    name = e["name"]
+    if name not in d or tuple(e["shape"]) != d[name].shape:
+      continue
+    rows = np.array(e["rows"], dtype=float)
+    np.testing.assert_allclose(d[name][:rows.shape[0], :rows.shape[1]], rows, atol=5e-5)
+    checked.add(name)
+  assert {"Dr", "LIFT", "x", "Fscale", "vmapM", "vmapP", "EToE", "EToF", "Fmask", "mapB",
+          "vmapB", "rk4a", "rx", "nx", "Fx", "V", "mapI", "mapO"} <= checked
