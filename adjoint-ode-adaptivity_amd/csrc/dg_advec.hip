@@ -89,8 +89,11 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
   for (int st = 0; st < MS; ++st) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const int fL = G::kFB + (s & 1) * 2 * (T + 2);  // faceL = lds[fL ...], faceR = lds[fR ...]
-      const int fR = fL + (T + 2);
+      // Face buffers alternate over the global stage index: consecutive stages (also across
+      // steps, where no barrier separates the last stage's reads from the next writes)
+      // never share one.
+      const int fL = G::kFB + ((st * NS + s) & 1) * 2 * (T + 2);  // faceL = lds[fL ...]
+      const int fR = fL + (T + 2);  // faceR = lds[fR ...]
       double u0[EPL], uN[EPL];
       double pe[EPL][NE], po[EPL][NO];
 #pragma unroll

@@ -94,13 +94,15 @@ template <int NP> struct NLGeo {
 // troubled, else 4 | (the active minmod argument, 0..3).  iin: LDS slot of the stage's
 // inflow flux f(uin).  Barriers: one (faces), two with the limiter (cell averages).
 template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE>
-__device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s, int iin,
+__device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s, int par, int iin,
                                         const Elem& E, double sc, const EOArgs<NP>& op,
                                         const LimEO<NP>& lc, double* ev, double* od,
                                         double* re, double* ro) {
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, T = kBlock;
   constexpr int FA = NLGeo<NP>::FA;
-  const int fL = (s & 1) * 2 * (T + 2), fR = fL + (T + 2);
+  // par: face buffer, alternating over consecutive stages (across steps too: without the
+  // limiter no barrier separates a step's last face reads from the next step's writes)
+  const int fL = par * 2 * (T + 2), fR = fL + (T + 2);
   double fe[NE], fo[NO];
   flux_eo<NP, BURG>(ev, od, fe, fo);
   const double f0 = fe[0] + fo[0], fN = fe[0] - fo[0];
@@ -265,8 +267,8 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
   for (int st = 0; st < MS; ++st) {
 #pragma unroll
     for (int s = 0; s < 5; ++s)
-      nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, CB + st * 5 + s, E, sc, args.op, args.lc,
-                                         ev, od, re, ro);
+      nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, (st * 5 + s) & 1, CB + st * 5 + s, E, sc,
+                                         args.op, args.lc, ev, od, re, ro);
     if (snap != nullptr || st == MS - 1) {
       __syncthreads();  // the last stage's exchange reads are done before the image is rewritten
       put_interior<NP, H>(lds, ev, od, false);
@@ -377,7 +379,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
       for (int k = 0; k < NE; ++k) se[s][k] = ev[k];
 #pragma unroll
       for (int k = 0; k < NO; ++k) so[s][k] = od[k];
-      const int c = nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, CB + s, E, sc, args.op,
+      const int c = nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, s & 1, CB + s, E, sc, args.op,
                                                        args.lc, ev, od, re, ro);
       if constexpr (LIM) codes |= c << (3 * s);
     }
