@@ -72,6 +72,10 @@ class EnsembleSweep:
 
   def adjoint(self):
     self.eta.zero_()
+    self.run_adjoint()
+
+  def run_adjoint(self):
+    """The adjoint kernels alone (eta already zeroed by the caller)."""
     self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta)
 
   def capture(self):

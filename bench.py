@@ -28,6 +28,7 @@ if ROOT not in sys.path:
   sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec peak (AMD data sheet; not in the guide)
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -52,10 +53,31 @@ def parse():
   return p.parse_args()
 
 
-def cpu_baseline(N, K, nsteps):
+def stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
+  """Achievable HBM bandwidth on this box: a device-to-device copy of
+  `nbytes` (read + write counted), median over `reps`, timed with HIP events."""
+  import torch
+  src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
+  dst = torch.empty_like(src)
+  st = torch.cuda.current_stream(dev)
+  dst.copy_(src)
+  ts = []
+  for _ in range(reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    dst.copy_(src)
+    e1.record(st)
+    e1.synchronize()
+    ts.append(e0.elapsed_time(e1) * 1e-3)
+  del src, dst
+  return 2.0 * nbytes / float(np.median(ts)) / 1e9
+
+
+def cpu_baseline(N, K, nsteps, threads=1):
   """The oracle (numpy restatement of utils/*.m + One_code.mlx, vectorised like MATLAB,
-  one thread) on a bounded sample of the same workload: `nsteps` forward + adjoint
-  steps at the full N, K."""
+  `threads` BLAS/OpenMP threads) on a bounded sample of the same workload: `nsteps`
+  forward + adjoint steps at the full N, K.  SURVEY §8d asks for 1 and 8 threads; only
+  the Dr/LIFT products are threaded by numpy, the elementwise passes stay serial."""
   from threadpoolctl import threadpool_limits
 
   from oracle import adjoint as oadj
@@ -65,15 +87,15 @@ def cpu_baseline(N, K, nsteps):
   a = 2 * np.pi
   dt = oadv.bench_dt(S)
   u0 = np.sin(2 * np.pi * S["x"])
-  with threadpool_limits(1):
+  with threadpool_limits(threads):
     t0 = time.perf_counter()
     snaps, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, a, S)
     oadj.adjoint_sweep(snaps[-1], snaps, times, dt, a, S)
     el = time.perf_counter() - t0
   dofs = 2 * (N + 1) * K * nsteps
-  return {"value": dofs / el, "unit": "DOF-updates/s", "cores": 1, "kind": "port",
+  return {"value": dofs / el, "unit": "DOF-updates/s", "cores": threads, "kind": "port",
           "sample": f"{nsteps} fwd + {nsteps} adj LSERK4 steps (with DWR indicator) at N={N}, "
-                    f"K={K}, numpy oracle, 1 thread, {el:.1f} s"}
+                    f"K={K}, numpy oracle, {threads} thread(s), {el:.1f} s"}
 
 
 def cpu_baseline_config3(N, K, nsteps):
@@ -236,8 +258,15 @@ def main():
     sweep.forward_graph() if args.graph else sweep.forward()
     if ev:
       ev[1].record(stream)
-      ev[2].record(stream)
-    sweep.adjoint_graph() if args.graph else sweep.adjoint()
+    if args.graph:
+      if ev:
+        ev[2].record(stream)
+      sweep.adjoint_graph()
+    else:  # eta's zero fill stays outside the adjoint kernels' bracket
+      sweep.eta.zero_()
+      if ev:
+        ev[2].record(stream)
+      sweep.run_adjoint()
     if ev:
       ev[3].record(stream)
     partial = sweep.reduce()
@@ -313,6 +342,9 @@ def main():
   # DOF-updates, so its HBM roofline is 8 TB/s / that per-update average.
   single_step_bytes = (16.0 + 24.0 + 16.0 / Np) / 2.0
   single_step_roofline = HBM_PEAK_GBS * 1e9 / single_step_bytes * world
+  # SURVEY §8d's algorithmic flop count, 5 (2 Np + 11) per DOF-update (both directions).
+  flop_per_update = 5.0 * (2 * Np + 11)
+  copy_gbs = stream_copy_gbs(dev) if rank == 0 else None
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
       "value": value,
@@ -343,11 +375,19 @@ def main():
       "single_step_roofline": {"value": single_step_roofline, "unit": "DOF-updates/s",
                                "bytes_per_update": single_step_bytes,
                                "frac": value / single_step_roofline},
+      "flops": {"per_dof_update": flop_per_update,
+                "achieved_tflops": value * flop_per_update / 1e12,
+                "peak_fp64_vector_tflops_per_gpu": FP64_PEAK_TFLOPS,
+                "frac": value * flop_per_update / 1e12 / (FP64_PEAK_TFLOPS * world)},
+      "stream_copy": {"achievable_GBs": copy_gbs, "unit": "GB/s",
+                      "what": "1 GiB device-to-device copy, read + write, rank 0",
+                      "adj_frac_of_achievable": adj_gbs / copy_gbs if copy_gbs else None},
       "steps_per_launch": ms,
       "refine_index": ref_idx,
   }
   if rank == 0 and world == 1 and args.ics == 0 and not args.no_cpu_baseline:
     out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_steps)
+    out["cpu_baseline_8t"] = cpu_baseline(N, K, args.cpu_steps, threads=8)
   if rank == 0:
     print(json.dumps(out), flush=True)
   if world > 1:

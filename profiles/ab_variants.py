@@ -23,8 +23,11 @@ def main():
   p.add_argument("--nsteps", type=int, default=20)
   p.add_argument("--rounds", type=int, default=5)
   p.add_argument("--variants", default="1:4:1,1:4:0,2:4:1,2:4:0,1:2:1,2:2:1")
+  p.add_argument("--lib", default=None, help="load this libdgadv.so instead (experiment builds)")
   a = p.parse_args()
   pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
+  if a.lib:
+    pkg._lib.LIB_PATH = os.path.abspath(a.lib)
   mesh = pkg.BaseGalerkin1D(n=a.N, k=a.K)
   op = pkg.operators.DGAdvection1D(mesh)
   dt = mesh.cfl_dt()
