@@ -36,13 +36,17 @@ def build(force=False, verbose=True, extra_flags=()):
   os.makedirs(objdir, exist_ok=True)
   flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-I", INCLUDE, *extra_flags]
   procs, objs = [], []
+  shared = max(os.path.getmtime(d) for d in deps[len(SRCS):])
   for src in SRCS:
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
+    objs.append(obj)
+    if (not force and not extra_flags and os.path.exists(obj)
+        and os.path.getmtime(obj) >= max(os.path.getmtime(src), shared)):
+      continue  # this translation unit is up to date
     cmd = [hipcc(), *flags, "-c", "-o", obj, src]
     if verbose:
       print("[build_ext]", " ".join(cmd))
     procs.append((subprocess.Popen(cmd), src))
-    objs.append(obj)
   failed = [src for p, src in procs if p.wait() != 0]
   if failed:
     raise RuntimeError(f"hipcc failed on {failed}; {OUT} was NOT updated")

@@ -478,7 +478,9 @@ __device__ __forceinline__ double minmod3(double a, double b, double c) {
   return 0.0;
 }
 
-template <int NP>
+// PI1: SlopeLimit1 (utils/SlopeLimit1.m:6-22) — the same projection and SlopeLimitLin
+// on every cell, without the troubled-cell test.
+template <int NP, bool PI1>
 __global__ __launch_bounds__(kBlock) void k_limit(const double* __restrict__ u,
                                                   double* __restrict__ ulim,
                                                   int32_t* __restrict__ ids,
@@ -517,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void k_limit(const double* __restrict__ u,
   const double ve1 = vk - minmod3(vk - ue1, vk - vkm1, vkp1 - vk);   // :21
   const double ve2 = vk + minmod3(ue2 - vk, vk - vkm1, vkp1 - vk);   // :22
   const double eps0 = 1.0e-8;
-  const bool flag = (fabs(ve1 - ue1) > eps0) || (fabs(ve2 - ue2) > eps0);  // :23
+  const bool flag = PI1 || (fabs(ve1 - ue1) > eps0) || (fabs(ve2 - ue2) > eps0);  // :23
 
   double out[NP];
 #pragma unroll
@@ -1007,7 +1009,8 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
 int dg_plan_set_physics(dg_plan* p, int flux, int limiter) {
   if (!p) return fail(DG_ERR_ARG, "null plan");
   if (flux != DG_FLUX_LINEAR && flux != DG_FLUX_BURGERS) return fail(DG_ERR_ARG, "bad flux");
-  if (limiter != DG_LIMIT_NONE && limiter != DG_LIMIT_EACH_STAGE)
+  if (limiter != DG_LIMIT_NONE && limiter != DG_LIMIT_EACH_STAGE &&
+      limiter != DG_LIMIT_PI1_EACH_STAGE)
     return fail(DG_ERR_ARG, "bad limiter");
   if ((flux != DG_FLUX_LINEAR || limiter != DG_LIMIT_NONE) && p->scheme != DG_TIME_LSERK4)
     return fail(DG_ERR_ARG, "nonlinear flux and the per-stage limiter need DG_TIME_LSERK4");
@@ -1177,8 +1180,19 @@ int dg_slope_limit_n(dg_plan* p, const double* u, double* ulim, int32_t* ids, vo
   if (u == ulim) return fail(DG_ERR_ARG, "in-place limiting is not supported (tiles overlap)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const unsigned grid = grid_for(p->ktot, kBlock - 2);
-  DG_DISPATCH_NP(p->NP, hipLaunchKernelGGL((k_limit<NP>), dim3(grid), dim3(kBlock), 0, st, u,
-                                           ulim, ids, p->d_VX, make_lim<NP>(p)));
+  DG_DISPATCH_NP(p->NP, hipLaunchKernelGGL((k_limit<NP, false>), dim3(grid), dim3(kBlock), 0, st,
+                                           u, ulim, ids, p->d_VX, make_lim<NP>(p)));
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+int dg_slope_limit_1(dg_plan* p, const double* u, double* ulim, void* stream) {
+  if (!p || !u || !ulim) return fail(DG_ERR_ARG, "null argument");
+  if (u == ulim) return fail(DG_ERR_ARG, "in-place limiting is not supported (tiles overlap)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned grid = grid_for(p->ktot, kBlock - 2);
+  DG_DISPATCH_NP(p->NP, hipLaunchKernelGGL((k_limit<NP, true>), dim3(grid), dim3(kBlock), 0, st,
+                                           u, ulim, nullptr, p->d_VX, make_lim<NP>(p)));
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }

@@ -34,6 +34,7 @@ template <int NP> struct LimEO {
   double V00;               // cell average = V(1,1) uh(1)
   double dv0, dv1;          // (Dr*ul)(1) = dv0 uh(1) + dv1 uh(2)             (SlopeLimitLin.m:16)
   double rce[NE], rco[NO];  // r_i / 2 in even/odd form: y = v + r/2 hm
+  int32_t every;            // SlopeLimit1 (SlopeLimit1.m:21): every cell limited, no test
 };
 
 // minmod (utils/minmod.m:6-12) of three values and which one it returned: 1..3, or 0 when
@@ -170,7 +171,7 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
     // Neighbour averages, replicated at a trajectory's ends (SlopeLimitN.m:18).
     const double am = lds[EDGE && E.first ? FA + el + 1 : FA + el];
     const double ap = lds[EDGE && E.last ? FA + el + 1 : FA + el + 2];
-    if (!troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0])) return 0;
+    if (!lc.every && !troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0])) return 0;
     double uh1 = lc.a1e[0] * ev[0];
 #pragma unroll
     for (int k = 1; k < NE; ++k) uh1 = fma(lc.a1e[k], ev[k], uh1);
@@ -646,6 +647,7 @@ template <int NP> LimEO<NP> make_lim_eo(const dg_plan* p) {
   }
   c.dv0 = d0;
   c.dv1 = d1;
+  c.every = p->limiter == DG_LIMIT_PI1_EACH_STAGE;
   return c;
 }
 

@@ -34,6 +34,8 @@ from .galerkin import BaseGalerkin1D
 INFLOW = {"a": _lib.DG_INFLOW_SIN_AT, "a2": _lib.DG_INFLOW_SIN_A2T}
 SCHEME = {"lserk4": _lib.DG_TIME_LSERK4, "euler": _lib.DG_TIME_EULER}
 FLUX = {"linear": _lib.DG_FLUX_LINEAR, "burgers": _lib.DG_FLUX_BURGERS}
+LIMITER = {False: _lib.DG_LIMIT_NONE, True: _lib.DG_LIMIT_EACH_STAGE,
+           "N": _lib.DG_LIMIT_EACH_STAGE, "1": _lib.DG_LIMIT_PI1_EACH_STAGE}
 
 
 def _stream(device):
@@ -51,7 +53,8 @@ class DGAdvection1D:
     inflow: "a" (uin = -sin(a t), AdvecRHS1D.m:14) or "a2" (-sin(a^2 t), One_code.mlx:129).
     time_scheme: "lserk4" (Globals1D.m:19-34) or "euler".
     flux: "linear" (a*u, AdvecRHS1D) or "burgers" (a*u^2/2, build-defined, config 3).
-    limiter: apply SlopeLimitN (utils/SlopeLimitN.m) after every LSERK4 stage.
+    limiter: after every LSERK4 stage apply SlopeLimitN (True or "N", utils/SlopeLimitN.m)
+      or SlopeLimit1 ("1", utils/SlopeLimit1.m: every cell limited); False: none.
   """
 
   def __init__(self, mesh, a=2 * np.pi, batch=1, inflow="a", time_scheme="lserk4",
@@ -82,9 +85,12 @@ class DGAdvection1D:
     self._plan = handle
     self._lib = lib
     self.flux = flux
+    if limiter not in LIMITER:
+      raise ValueError(f"limiter must be one of {sorted(LIMITER, key=str)}, got {limiter!r}")
     self.limiter = bool(limiter)
+    self.limiter_kind = {0: None, 1: "N", 2: "1"}[LIMITER[limiter]]
     if flux != "linear" or limiter:
-      _lib.check(lib.dg_plan_set_physics(handle, FLUX[flux], int(bool(limiter))),
+      _lib.check(lib.dg_plan_set_physics(handle, FLUX[flux], LIMITER[limiter]),
                  "dg_plan_set_physics")
     self._query()
     self._idx = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -227,6 +233,14 @@ class DGAdvection1D:
     rc = self._lib.dg_slope_limit_n(self._plan, self._field(u, "u"), self._field(out, "out"),
                                     ids_p, _stream(self.device))
     _lib.check(rc, "dg_slope_limit_n")
+    return out
+
+  def slope_limit_1(self, u, out=None):
+    """SlopeLimit1(u) (utils/SlopeLimit1.m:1-23): the Pi^1 limiter on every element."""
+    out = torch.empty_like(u) if out is None else out
+    rc = self._lib.dg_slope_limit_1(self._plan, self._field(u, "u"), self._field(out, "out"),
+                                    _stream(self.device))
+    _lib.check(rc, "dg_slope_limit_1")
     return out
 
   def argmax_async(self, x, use_abs=True, out=None):

@@ -100,13 +100,15 @@ int dg_plan_tune(dg_plan* plan, int key, int64_t value);
  *                       on f and inflow f(uin) (build-defined, BASELINE config 3, SURVEY 8d;
  *                       CPU statement oracle/burgers.py)
  *   DG_LIMIT_EACH_STAGE u = SlopeLimitN(u) (utils/SlopeLimitN.m:1-33) after every stage update
+ *   DG_LIMIT_PI1_EACH_STAGE  u = SlopeLimit1(u) (utils/SlopeLimit1.m:1-23, every cell limited)
+ *                       after every stage update
  * Both need DG_TIME_LSERK4.  With either, dg_advec_rhs evaluates the flux's RHS (no limiter),
  * dg_lserk4_fwd runs limited steps (at most 2 per launch), and dg_lserk4_adj is the exact
  * transpose of each step's tangent at the stored forward states, with the limiter's discrete
  * decisions (troubled cells, active minmod argument) frozen; it recomputes step n's stages from
  * snapshots[n] (one launch per step) and takes the indicator residual of the flux f. */
 enum { DG_FLUX_LINEAR = 0, DG_FLUX_BURGERS = 1 };
-enum { DG_LIMIT_NONE = 0, DG_LIMIT_EACH_STAGE = 1 };
+enum { DG_LIMIT_NONE = 0, DG_LIMIT_EACH_STAGE = 1, DG_LIMIT_PI1_EACH_STAGE = 2 };
 int dg_plan_set_physics(dg_plan* plan, int flux, int limiter);
 
 /* Grow the plan's device mesh and scratch buffers to hold K_capacity elements per trajectory,
@@ -159,6 +161,10 @@ int dg_lserk4_adj(dg_plan* plan, double* w, const double* snapshots, double t0, 
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */
 int dg_slope_limit_n(dg_plan* plan, const double* u, double* ulim, int32_t* ids_mask,
                      void* stream);
+
+/* ulim = SlopeLimit1(u)  — utils/SlopeLimit1.m:1-23: the Pi^1 limiter (linear projection +
+ * SlopeLimitLin) on every element, no troubled-cell test. */
+int dg_slope_limit_1(dg_plan* plan, const double* u, double* ulim, void* stream);
 
 /* idx[0] = argmax(x[0:n]) (or of |x| when use_abs), first index on ties, NaN counts as
  * maximum — numpy.argmax semantics used at python/Main_finite_difference.py:337.

@@ -30,7 +30,7 @@ definition, oracle/adjoint.py, with f in place of a*u).
 import numpy as np
 
 from .advec import INFLOW_A, face_jumps, inflow_value
-from .limiter import _row_dot, cell_average, minmod, slope_limit_n
+from .limiter import _row_dot, cell_average, minmod, slope_limit_1, slope_limit_n
 from .setup1d import RK4A, RK4B, RK4C
 
 FLUX_LINEAR = "linear"
@@ -71,10 +71,19 @@ def rhs_tangent(u, du, a, S, kind=FLUX_BURGERS):
 # ---------------------------------------------------------------------------
 # Limited LSERK4 step
 # ---------------------------------------------------------------------------
+def _limit(v, S, limit):
+  """The stage limiter: limit True / "N" = SlopeLimitN (troubled cells only), "1" =
+  SlopeLimit1 (utils/SlopeLimit1.m: every cell).  Returns (u, limited cell indices)."""
+  if limit == "1":
+    return slope_limit_1(v, S), np.arange(v.shape[1])
+  return slope_limit_n(v, S, return_ids=True)
+
+
 def limited_step(u, time, dt, a, S, kind=FLUX_BURGERS, inflow=INFLOW_A, limit=True,
                  return_ids=False):
-  """One LSERK4 step (One_code.mlx:120-137) with u = SlopeLimitN(u) after every stage.
-  return_ids: also the list of the 5 troubled-cell index arrays."""
+  """One LSERK4 step (One_code.mlx:120-137) with u = SlopeLimitN(u) (limit True or "N") or
+  u = SlopeLimit1(u) (limit "1") after every stage.
+  return_ids: also the list of the 5 limited-cell index arrays."""
   resu = np.zeros_like(u)
   ids_all = []
   for s in range(5):
@@ -82,7 +91,7 @@ def limited_step(u, time, dt, a, S, kind=FLUX_BURGERS, inflow=INFLOW_A, limit=Tr
     resu = RK4A[s] * resu + dt * rhsu
     v = u + RK4B[s] * resu
     if limit:
-      u, ids = slope_limit_n(v, S, return_ids=True)
+      u, ids = _limit(v, S, limit)
       ids_all.append(ids)
     else:
       u = v
@@ -109,10 +118,11 @@ def _neighbours(v):
   return np.concatenate(([v[0]], v[:K - 1])), np.concatenate((v[1:], [v[K - 1]]))  # :18
 
 
-def slope_limit_n_jvp(v, dv, S):
+def slope_limit_n_jvp(v, dv, S, limit=True):
   """(SlopeLimitN(v), its derivative applied to dv) with the troubled-cell set and the
-  active minmod argument frozen at v (first index on ties, as minmod's min)."""
-  y, ids = slope_limit_n(v, S, return_ids=True)
+  active minmod argument frozen at v (first index on ties, as minmod's min).  limit "1":
+  the same for SlopeLimit1 (every cell limited)."""
+  y, ids = _limit(v, S, limit)
   dy = dv.copy()
   if ids.size == 0:
     return y, dy
@@ -154,7 +164,7 @@ def step_jvp(u, du, time, dt, a, S, kind=FLUX_BURGERS, inflow=INFLOW_A, limit=Tr
     v = u + RK4B[s] * resu
     dv = du + RK4B[s] * dres
     if limit:
-      u, du = slope_limit_n_jvp(v, dv, S)
+      u, du = slope_limit_n_jvp(v, dv, S, limit)
     else:
       u, du = v, dv
   return u, du

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 RTOL = 1e-10
 A = 2 * np.pi
-PHYSICS = [("burgers", True), ("burgers", False), ("linear", True)]
+PHYSICS = [("burgers", True), ("burgers", False), ("linear", True), ("burgers", "1")]
 
 
 def rel_err(x, ref):
@@ -137,7 +137,7 @@ def test_adjoint_sweep_and_indicator(pkg, gpu, flux, limit, N, K, uniform):
   assert rel_err(host(eta), eta_ref) <= RTOL
 
 
-@pytest.mark.parametrize("limit", [False, True])
+@pytest.mark.parametrize("limit", [False, True, "1"])
 def test_gradient_matches_finite_difference(pkg, gpu, limit):
   """dJ/du0 through 4 limited Burgers steps vs a central difference of J on the GPU
   (matlab/test_jacobian.m:38-55 method).  With the limiter the step is only piecewise

@@ -260,6 +260,19 @@ def test_slope_limiter_matches_SlopeLimitN(pkg, gpu, N):
   np.testing.assert_allclose(setup1d.from_elem_major(got, N + 1), ref, rtol=0, atol=1e-13)
 
 
+@pytest.mark.parametrize("N", [1, 2, 4, 8])
+def test_slope_limiter_matches_SlopeLimit1(pkg, gpu, N):
+  """dg_slope_limit_1 vs utils/SlopeLimit1.m (every cell limited), same summation order."""
+  rng = np.random.default_rng(100 + N)
+  K = 517
+  S, mesh = mesh_pair(pkg, N, K)
+  u = _limiter_input(rng, S)
+  ref = olim.slope_limit_1(u, S)
+  op = make_op(pkg, mesh)
+  got = host(op.slope_limit_1(dev(setup1d.to_elem_major(u), gpu)))
+  np.testing.assert_allclose(setup1d.from_elem_major(got, N + 1), ref, rtol=0, atol=1e-13)
+
+
 # ---------------------------------------------------------------------------
 def test_argmax_numpy_semantics(pkg, gpu):
   S, mesh = mesh_pair(pkg, 2, 4000)

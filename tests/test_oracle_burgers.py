@@ -56,7 +56,7 @@ def test_burgers_rhs_is_conservative_and_consistent():
 
 
 @pytest.mark.parametrize("kind", [ob.FLUX_BURGERS, ob.FLUX_LINEAR])
-@pytest.mark.parametrize("limit", [False, True])
+@pytest.mark.parametrize("limit", [False, True, "1"])
 def test_step_tangent_matches_central_difference(kind, limit):
   rng = np.random.default_rng(2)
   S = setup1d.uniform_setup(3, 12, metric="element")
@@ -73,7 +73,7 @@ def test_step_tangent_matches_central_difference(kind, limit):
 
 
 @pytest.mark.parametrize("kind,limit", [(ob.FLUX_BURGERS, True), (ob.FLUX_BURGERS, False),
-                                        (ob.FLUX_LINEAR, True)])
+                                        (ob.FLUX_LINEAR, True), (ob.FLUX_BURGERS, "1")])
 def test_coloured_adjoint_equals_dense_transpose(kind, limit):
   rng = np.random.default_rng(3)
   S = setup1d.uniform_setup(2, 25, metric="element")  # K > 21: real colouring
@@ -100,7 +100,7 @@ def test_linear_unlimited_adjoint_is_the_linear_adjoint():
   np.testing.assert_allclose(got, oadj.adjoint_step(w, dt, A, S), atol=1e-13)
 
 
-@pytest.mark.parametrize("limit", [False, True])
+@pytest.mark.parametrize("limit", [False, True, "1"])
 def test_adjoint_sweep_gradient_matches_finite_difference(limit):
   """dJ/du0 for J = <g, u^N> + src/2 sum |u^n|^2 through 3 limited Burgers steps."""
   rng = np.random.default_rng(5)
