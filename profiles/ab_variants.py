@@ -24,12 +24,15 @@ def main():
   p.add_argument("--rounds", type=int, default=5)
   p.add_argument("--variants", default="1:4:1,1:4:0,2:4:1,2:4:0,1:2:1,2:2:1")
   p.add_argument("--lib", default=None, help="load this libdgadv.so instead (experiment builds)")
+  p.add_argument("--flux", default="linear", choices=("linear", "burgers"))
+  p.add_argument("--limiter", default="0", choices=("0", "N", "1"))
   a = p.parse_args()
   pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
   if a.lib:
     pkg._lib.LIB_PATH = os.path.abspath(a.lib)
   mesh = pkg.BaseGalerkin1D(n=a.N, k=a.K)
-  op = pkg.operators.DGAdvection1D(mesh)
+  op = pkg.operators.DGAdvection1D(mesh, flux=a.flux,
+                                   limiter={"0": False, "N": "N", "1": "1"}[a.limiter])
   dt = mesh.cfl_dt()
   snaps = op.new_field(a.nsteps + 1)
   op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
