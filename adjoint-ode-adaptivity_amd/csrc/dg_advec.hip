@@ -1094,10 +1094,14 @@ int dg_lserk4_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, doubl
                   void* stream) {
   if (!p || !u) return fail(DG_ERR_ARG, "null argument");
   if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
-  if (nsteps == 0) return DG_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (p->nonlinear()) return nl_fwd(p, u, t0, dt, nsteps, snapshots, st);
   const int64_t field = p->ktot * p->NP;
+  if (nsteps == 0) {  // the empty sweep: snapshot 0 still receives u^0
+    if (snapshots && snapshots != u)
+      HIP_TRY(hipMemcpyAsync(snapshots, u, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
+    return DG_OK;
+  }
+  if (p->nonlinear()) return nl_fwd(p, u, t0, dt, nsteps, snapshots, st);
   // Time levels by repeated addition (time = time + dt, One_code.mlx:139).
   std::vector<double> tn(size_t(nsteps) + 1);
   tn[0] = t0;
