@@ -46,6 +46,8 @@ def main():
       e0.record(st)
       if a.what == "fwd":
         op.forward(u, 0.0, dt, a.ms)
+      elif a.what == "fwdsnap":  # one launch writing ms snapshots, no copies in the bracket
+        op.forward(snaps[0], 0.0, dt, a.ms, snaps)
       else:
         op.adjoint(u, snaps, 0.0, dt, a.ms, eta=eta)
       e1.record(st)
