@@ -1014,6 +1014,20 @@ int dg_plan_set_physics(dg_plan* p, int flux, int limiter) {
     return fail(DG_ERR_ARG, "bad limiter");
   if ((flux != DG_FLUX_LINEAR || limiter != DG_LIMIT_NONE) && p->scheme != DG_TIME_LSERK4)
     return fail(DG_ERR_ARG, "nonlinear flux and the per-stage limiter need DG_TIME_LSERK4");
+  if (limiter != DG_LIMIT_NONE) {
+    // The limiter kernels use the LGL symmetry (dg_burgers.hip LimEO): row 1 of invV even,
+    // row 2 odd, r odd.
+    const int NP = p->NP, N = NP - 1;
+    double worst = 0.0;
+    for (int k = 0; k < NP; ++k) {
+      worst = std::max(worst, std::fabs(p->invV[k] - p->invV[N - k]));
+      worst = std::max(worst, std::fabs(p->invV[NP + k] + p->invV[NP + N - k]));
+      worst = std::max(worst, std::fabs(p->r[k] + p->r[N - k]));
+    }
+    if (!(worst <= 1e-13))
+      return fail(DG_ERR_ARG, "the limiter needs symmetric LGL nodes (asymmetry " +
+                                  std::to_string(worst) + ")");
+  }
   p->flux = flux;
   p->limiter = limiter;
   return DG_OK;

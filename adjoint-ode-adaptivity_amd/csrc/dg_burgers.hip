@@ -26,14 +26,16 @@
 namespace {
 using namespace dgk;
 
-// Limiter constants in even/odd coordinates (host: make_lim_eo).
+// Limiter constants in even/odd coordinates (host: make_lim_eo).  The LGL nodes are
+// symmetric, so row 1 of invV (P0) is even, row 2 (P1) odd and r odd: the parts that
+// vanish in exact arithmetic (the odd part of row 1, the even part of row 2, the even part
+// of r) are dropped; dg_plan_set_physics checks that they are below 1e-13.
 template <int NP> struct LimEO {
   static constexpr int NE = (NP + 1) / 2, NO = NP / 2;
-  double a0e[NE], a0o[NO];  // uh(1) = sum_j invV(1,j) v_j = a0e.e + a0o.o   (SlopeLimitN.m:9)
-  double a1e[NE], a1o[NO];  // uh(2) = sum_j invV(2,j) v_j                    (SlopeLimitN.m:28)
-  double V00;               // cell average = V(1,1) uh(1)
-  double dv0, dv1;          // (Dr*ul)(1) = dv0 uh(1) + dv1 uh(2)             (SlopeLimitLin.m:16)
-  double rce[NE], rco[NO];  // r_i / 2 in even/odd form: y = v + r/2 hm
+  double a0e[NE];           // cell average V(1,1) uh(1), uh(1) = sum_j invV(1,j) v_j  (SlopeLimitN.m:9)
+  double a1o[NO];           // uh(2) = sum_j invV(2,j) v_j = a1o.o             (SlopeLimitN.m:28)
+  double dv0, dv1;          // h ux(1) = 2 (Dr*ul)(1) = dv0 avg + dv1 uh(2)  (SlopeLimitLin.m:16)
+  double rco[NO];           // r_i / 2, odd part: y = v + r/2 hm
   int32_t every;            // SlopeLimit1 (SlopeLimit1.m:21): every cell limited, no test
 };
 
@@ -57,12 +59,17 @@ __device__ __forceinline__ double minmod_br(double a, double b, double c, int& b
   return pos ? m : -m;
 }
 
-// The troubled-cell test of SlopeLimitN.m:21-23.
+// The troubled-cell test of SlopeLimitN.m:21-23.  Both minmods share the neighbour
+// differences b = v - v-, c = v+ - v; with all three arguments of one sign minmod is their
+// min (all > 0) or max (all < 0), exactly as s*min|.| (minmod.m:9-11), else 0.
 __device__ __forceinline__ bool troubled(double v, double vm, double vp, double u0, double uN) {
-  int br;
-  const double ve1 = v - minmod_br(v - u0, v - vm, vp - v, br);
-  const double ve2 = v + minmod_br(uN - v, v - vm, vp - v, br);
-  return fabs(ve1 - u0) > 1.0e-8 || fabs(ve2 - uN) > 1.0e-8;
+  const double b = v - vm, c = vp - v;
+  const bool bcp = b > 0.0 && c > 0.0, bcn = b < 0.0 && c < 0.0;
+  const double mn = fmin(b, c), mx = fmax(b, c);
+  const double a1 = v - u0, a2 = uN - v;
+  const double m1 = (bcp && a1 > 0.0) ? fmin(a1, mn) : ((bcn && a1 < 0.0) ? fmax(a1, mx) : 0.0);
+  const double m2 = (bcp && a2 > 0.0) ? fmin(a2, mn) : ((bcn && a2 < 0.0) ? fmax(a2, mx) : 0.0);
+  return fabs((v - m1) - u0) > 1.0e-8 || fabs((v + m2) - uN) > 1.0e-8;
 }
 
 // Flux values divided by a, in even/odd coordinates: f = u (linear) or u^2/2 (Burgers):
@@ -160,27 +167,22 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
   if constexpr (!LIM) {
     return 0;
   } else {
-    double uh0 = lc.a0e[0] * ev[0];
+    double avg = lc.a0e[0] * ev[0];
 #pragma unroll
-    for (int k = 1; k < NE; ++k) uh0 = fma(lc.a0e[k], ev[k], uh0);
-#pragma unroll
-    for (int k = 0; k < NO; ++k) uh0 = fma(lc.a0o[k], od[k], uh0);
-    const double avg = lc.V00 * uh0;
+    for (int k = 1; k < NE; ++k) avg = fma(lc.a0e[k], ev[k], avg);
     lds[FA + el + 1] = avg;
     __syncthreads();
     // Neighbour averages, replicated at a trajectory's ends (SlopeLimitN.m:18).
     const double am = lds[EDGE && E.first ? FA + el + 1 : FA + el];
     const double ap = lds[EDGE && E.last ? FA + el + 1 : FA + el + 2];
     if (!lc.every && !troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0])) return 0;
-    double uh1 = lc.a1e[0] * ev[0];
+    double uh1 = lc.a1o[0] * od[0];
 #pragma unroll
-    for (int k = 1; k < NE; ++k) uh1 = fma(lc.a1e[k], ev[k], uh1);
-#pragma unroll
-    for (int k = 0; k < NO; ++k) uh1 = fma(lc.a1o[k], od[k], uh1);
+    for (int k = 1; k < NO; ++k) uh1 = fma(lc.a1o[k], od[k], uh1);
     int br;
-    const double hm = minmod_br(2.0 * fma(lc.dv0, uh0, lc.dv1 * uh1), ap - avg, avg - am, br);
+    const double hm = minmod_br(fma(lc.dv0, avg, lc.dv1 * uh1), ap - avg, avg - am, br);
 #pragma unroll
-    for (int k = 0; k < NE; ++k) ev[k] = fma(lc.rce[k], hm, avg);
+    for (int k = 0; k < NE; ++k) ev[k] = avg;
 #pragma unroll
     for (int k = 0; k < NO; ++k) od[k] = lc.rco[k] * hm;
     return 4 | br;
@@ -441,8 +443,6 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
         for (int k = 1; k < NE; ++k) ls += we[k];
         double mu = 0.0;  // adjoint of hm
 #pragma unroll
-        for (int k = 0; k < NE; ++k) mu = fma(args.lc.rce[k], we[k], mu);
-#pragma unroll
         for (int k = 0; k < NO; ++k) mu = fma(args.lc.rco[k], wo[k], mu);
         const int br = code & 3;
         cs = ls;
@@ -454,13 +454,12 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
           cs += mu;
           cl = -mu;
         }
-        const double g = (br == 1) ? 2.0 * mu : 0.0;
+        const double g = (br == 1) ? mu : 0.0;
+        const double g0 = g * args.lc.dv0, g1 = g * args.lc.dv1;
 #pragma unroll
-        for (int k = 0; k < NE; ++k)
-          we[k] = g * fma(args.lc.dv0, args.lc.a0e[k], args.lc.dv1 * args.lc.a1e[k]);
+        for (int k = 0; k < NE; ++k) we[k] = g0 * args.lc.a0e[k];
 #pragma unroll
-        for (int k = 0; k < NO; ++k)
-          wo[k] = g * fma(args.lc.dv0, args.lc.a0o[k], args.lc.dv1 * args.lc.a1o[k]);
+        for (int k = 0; k < NO; ++k) wo[k] = g1 * args.lc.a1o[k];
       }
       lds[CL + lane + 1] = cl;
       lds[CR + lane + 1] = cr;
@@ -469,11 +468,8 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
       // ends the replicated neighbour average is the cell's own (SlopeLimitN.m:18).
       const double alpha = cs + lds[EDGE && E.first ? CL + lane + 1 : CR + lane] +
                            lds[EDGE && E.last ? CR + lane + 1 : CL + lane + 2];
-      const double av = alpha * args.lc.V00;
 #pragma unroll
-      for (int k = 0; k < NE; ++k) we[k] = fma(av, args.lc.a0e[k], we[k]);
-#pragma unroll
-      for (int k = 0; k < NO; ++k) wo[k] = fma(av, args.lc.a0o[k], wo[k]);
+      for (int k = 0; k < NE; ++k) we[k] = fma(alpha, args.lc.a0e[k], we[k]);
     }
     const int f0 = (ss & 1) * 2 * (T + 2), f1 = f0 + (T + 2);
     double qe[NE], qo[NO];
@@ -628,25 +624,21 @@ template <int NP> LimEO<NP> make_lim_eo(const dg_plan* p) {
   const double* i1 = p->invV + NP;  // row 2
   for (int k = 0; k < NO; ++k) {
     c.a0e[k] = i0[k] + i0[N - k];
-    c.a0o[k] = i0[k] - i0[N - k];
-    c.a1e[k] = i1[k] + i1[N - k];
     c.a1o[k] = i1[k] - i1[N - k];
-    c.rce[k] = 0.25 * (p->r[k] + p->r[N - k]);
     c.rco[k] = 0.25 * (p->r[k] - p->r[N - k]);
   }
   if (NE > NO) {
     c.a0e[NO] = i0[NO];
-    c.a1e[NO] = i1[NO];
-    c.rce[NO] = 0.5 * p->r[NO];
   }
-  c.V00 = p->V[0];
+  const double V00 = p->V[0];  // V(1,1): the cell average is V(1,1) uh(1)
+  for (int k = 0; k < NE; ++k) c.a0e[k] *= V00;
   double d0 = 0.0, d1 = 0.0;
   for (int l = 0; l < NP; ++l) {
     d0 += p->Dr[l] * p->V[l * NP + 0];
     d1 += p->Dr[l] * p->V[l * NP + 1];
   }
-  c.dv0 = d0;
-  c.dv1 = d1;
+  c.dv0 = 2.0 * d0 / V00;  // uh(1) = avg / V(1,1)
+  c.dv1 = 2.0 * d1;
   c.every = p->limiter == DG_LIMIT_PI1_EACH_STAGE;
   return c;
 }
