@@ -10,7 +10,7 @@ Submodules:
   galerkin   host-side setup with the BaseGalerkin1D attribute surface (numpy)
   operators  DGAdvection1D: the HIP plan and its kernels (torch CUDA tensors)
   factory    Problem / Funs / AdaptFuns / AdaptState / FunFactory adapt-loop API
-  ensemble   ensembles of initial conditions sharded over ranks (RCCL all-gather)
+  ensemble   ensembles of initial conditions sharded over ranks (rank-ordered RCCL sum)
   adaptive   device-resident spatial adapt loop (config 3: fwd + adj + refine)
   dgtime     batched DG-in-time marches + DWR for ODE ensembles (matlab/MAIN.m loop)
   fd_ensemble  the finite-difference DWR adapt loop for ODE ensembles on the device

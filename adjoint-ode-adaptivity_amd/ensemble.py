@@ -5,10 +5,11 @@ The reference's only data-parallel axis is the ensemble of initial conditions
 an argmax (:479, :491).  Here each rank owns a contiguous block of ICs, runs the
 forward + adjoint sweeps for all of them as one batched plan (no data-path
 communication), reduces its per-IC indicators to one K-vector in fixed order, and the
-ranks exchange those partial sums with ONE all-gather (RCCL over xGMI on GPUs).  Every
-rank then sums the gathered slices in rank order, so the mean indicator and the refine
-index are bit-identical on all ranks regardless of the collective's internal order
-(an all-reduce would not guarantee that).
+ranks sum those partial sums in rank order with a reduce-scatter built from one
+all-to-all (each rank owns a 1/W slice and adds the W partials of it in rank order)
+and one all-gather of the summed slices (RCCL over xGMI on GPUs).  The mean indicator
+and the refine index are bit-identical on all ranks and independent of the
+collectives' internal order, which an RCCL all-reduce would not pin down.
 """
 import numpy as np
 import torch
@@ -131,20 +132,33 @@ class DeviceReducer:
 
 
 def gather_indicator(partial, n_total, reducer, group=None):
-  """All-gather the per-rank partial sums, sum them in rank order, take the mean over
+  """Sum the per-rank partial indicators over the ranks in rank order, take the mean over
   all ICs and the argmax of its magnitude (python/Main_width_ref.py:479,491).
-  Returns (mean indicator, index tensor).  Works for any world size (1 = no collective)."""
+  Returns (mean indicator, index tensor).  Works for any world size (1 = no collective).
+
+  The exchange is a rank-ordered reduce-scatter built from one all-to-all (rank j
+  receives every rank's partial for its slice j of the K values and sums them in rank
+  order) followed by an all-gather of the summed slices: 2 (W-1)/W K doubles in and out per
+  rank, like a ring all-reduce, instead of the (W-1) K of gathering every partial.  The
+  result is bit-identical on every rank and equal to summing the W partials in rank order."""
   if dist.is_available() and dist.is_initialized():
     world = dist.get_world_size(group)
   else:
     world = 1
   if world > 1:
-    bufs = [torch.empty_like(partial) for _ in range(world)]
-    dist.all_gather(bufs, partial.contiguous(), group=group)
-    stacked = torch.stack(bufs)
+    K = partial.numel()
+    chunk = -(-K // world)
+    send = partial.new_zeros(world * chunk)
+    send[:K] = partial.reshape(-1)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)  # recv row r: rank r's slice
+    mine = reducer.sum_rows(recv.view(world, chunk))  # rank order
+    full = torch.empty_like(send)
+    dist.all_gather_into_tensor(full, mine.contiguous(), group=group)
+    total = full[:K]
   else:
-    stacked = partial.reshape(1, -1)
-  # one slice: its sum is itself; dividing by 1 is exact (both shortcuts are bit-identical)
-  total = reducer.sum_rows(stacked) if stacked.shape[0] > 1 else partial
+    # one slice: its sum is itself
+    total = partial
+  # dividing by 1 is exact (bit-identical shortcut)
   mean = total / float(n_total) if n_total != 1 else total
   return mean, reducer.argmax(mean)

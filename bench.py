@@ -2,13 +2,13 @@
 
 One bench step = one forward sweep of --nsteps fused LSERK4 steps (snapshots stored),
 one adjoint sweep of --nsteps reverse steps accumulating the dual-weighted residual,
-the per-rank indicator reduction, the cross-rank all-gather + fixed-order sum + argmax
+the per-rank indicator reduction, the cross-rank rank-ordered sum (all-to-all + all-gather) + argmax
 (the refine decision), and the refine index copied to the host.
 
 Workload per rank = BASELINE config 2 (N=4, K=1,048,576, fp64, uniform mesh on [0,1],
 a = 2*pi, dt from One_code.mlx:111-112).  Rank 0 runs u0 = sin(2 pi x) (the golden IC);
 rank j > 0 runs IC j of the synthetic ensemble.  N GPUs = an ensemble of N
-trajectories, one per GPU (weak scaling; the only exchange is the indicator all-gather).
+trajectories, one per GPU (weak scaling; the only exchange is the indicator sum).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--nsteps S] [--no-cpu-baseline]
   python bench.py --config 3     BASELINE config 3: Burgers-type flux + SlopeLimitN after

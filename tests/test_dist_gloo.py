@@ -1,5 +1,6 @@
-"""The multi-rank exchange of the ensemble path (all-gather of per-rank partial
-indicator sums, rank-ordered sum, mean, argmax) on CPU with world_size 2 and 4 (gloo).
+"""The multi-rank exchange of the ensemble path (rank-ordered sum of the per-rank partial
+indicator sums by all-to-all + all-gather, mean, argmax) on CPU with world_size 2, 3 and 4
+(gloo), K not a multiple of the world size.
 
 The product reducer runs the HIP kernels (dg_sum_rows / dg_argmax) and needs a GPU; the
 exchange logic is the same function with the oracle's reducer plugged in here, and the
@@ -31,7 +32,7 @@ def _free_port():
     return s.getsockname()[1]
 
 
-def _partials(world, K=1000, n_ics=12):
+def _partials(world, K=1001, n_ics=12):
   """Per-IC indicator rows (deterministic), summed per rank in fixed order."""
   rng = np.random.default_rng(0)
   rows = rng.standard_normal((n_ics, K)) * 10.0 ** rng.integers(-6, 3, (n_ics, K))
@@ -60,7 +61,7 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_gather_indicator_rank_order_and_identical_on_all_ranks(world):
   mgr = mp.Manager()
   out = mgr.dict()
