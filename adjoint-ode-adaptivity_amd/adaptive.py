@@ -18,6 +18,16 @@ import torch
 from .operators import DGAdvection1D
 
 
+def check_indicator(value_at_refine_index, idx):
+  """Failure detection for the adapt loop: the refine index comes from an
+  argmax that ranks NaN and +-inf first, so the indicator is finite everywhere exactly
+  when it is finite there.  A non-finite indicator (a blown-up sweep, e.g. a time step
+  above the CFL limit) raises instead of refining element ``idx``."""
+  if not np.isfinite(value_at_refine_index):
+    raise FloatingPointError(f"non-finite DWR indicator ({value_at_refine_index}) at element "
+                             f"{idx}: the forward or adjoint sweep diverged")
+
+
 class AdaptiveSweep:
   """Fixed-step forward + adjoint sweeps and device refinement on one trajectory.
 
@@ -87,12 +97,15 @@ class AdaptiveSweep:
     iteration needs the step size."""
     dofs = 2 * self.op.Np * self.op.ktot * self.nsteps
     self.op.argmax_async(self.eta(), use_abs=True, out=self.idx)
+    # argmax puts NaN (and |inf|) first, so eta at the refine index is finite iff all are
+    self._eta_at = self._eta.index_select(0, self.idx)
     self.op.refine(self.idx, self.h_split)
     return dofs
 
   def sync(self):
     """Bring the refine index and the split width to the host; update h_min."""
     idx = int(self.idx.item())
+    check_indicator(float(self._eta_at.item()), idx)
     self.h_min = min(self.h_min, 0.5 * float(self.h_split.item()))
     self.history.append(idx)
     return idx

@@ -251,6 +251,7 @@ def main():
     sweep.capture()  # each sweep becomes one HIP graph launch
   stream = torch.cuda.current_stream(dev)
   idx_host = torch.zeros(1, dtype=torch.int64).pin_memory()
+  val_host = torch.zeros(1, dtype=torch.float64).pin_memory()
 
   def one_step(ev=None):
     if ev:
@@ -270,10 +271,12 @@ def main():
     if ev:
       ev[3].record(stream)
     partial = sweep.reduce()
-    _, idx = ens.gather_indicator(partial, n_total, reducer)
+    mean, idx = ens.gather_indicator(partial, n_total, reducer)
     # The refine index goes to the host (the mesh split's input) without stalling the
     # stream: an async copy into pinned memory, read once the timed region has synced.
+    # The indicator there is finite iff it is finite everywhere (argmax ranks NaN first).
     idx_host.copy_(idx, non_blocking=True)
+    val_host.copy_(mean.index_select(0, idx), non_blocking=True)
 
   for _ in range(args.warmup):
     one_step()
@@ -288,6 +291,7 @@ def main():
     one_step(evs[s])
   torch.cuda.synchronize()
   ref_idx = int(idx_host.item())
+  pkg.adaptive.check_indicator(float(val_host.item()), ref_idx)
   if world > 1:
     dist.barrier()
   torch.cuda.synchronize()

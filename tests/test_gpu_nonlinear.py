@@ -323,3 +323,12 @@ def test_adaptive_sweep_driver(pkg, gpu):
     v_x = pkg.split_interval(v_x, j)
     np.testing.assert_array_equal(run.op.v_x(), v_x)
   assert run.K == K0 + 5
+
+
+def test_diverged_sweep_is_refused(pkg, gpu):
+  """A time step far above the CFL limit blows the unlimited sweep up; the adapt loop
+  raises instead of refining on a NaN indicator."""
+  mesh = pkg.BaseGalerkin1D(n=4, k=64, domain=[0.0, 1.0])
+  run = pkg.adaptive.AdaptiveSweep(mesh, 300, 2, flux="linear", limiter=False, cfl=60.0)
+  with pytest.raises(FloatingPointError):
+    run.iterate()

@@ -173,3 +173,13 @@ def test_save_to_1d_global_data_roundtrip(pkg, tmp_path):
     checked.add(name)
   assert {"Dr", "LIFT", "x", "Fscale", "vmapM", "vmapP", "EToE", "EToF", "Fmask", "mapB",
           "vmapB", "rk4a", "rx", "nx", "Fx", "V", "mapI", "mapO"} <= checked
+
+
+def test_check_indicator_flags_non_finite(pkg):
+  """Failure detection: the refine decision refuses a non-finite indicator."""
+  import math
+  pkg.adaptive.check_indicator(1.5e-3, 7)
+  pkg.adaptive.check_indicator(0.0, 0)
+  for bad in (math.nan, math.inf, -math.inf):
+    with pytest.raises(FloatingPointError):
+      pkg.adaptive.check_indicator(bad, 3)
