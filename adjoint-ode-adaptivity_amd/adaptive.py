@@ -75,17 +75,24 @@ class AdaptiveSweep:
   def eta(self):
     return self._eta[:self.op.ktot]
 
-  def forward(self, dt=None):
-    snaps = self.snapshots()
+  def init_state(self):
+    """u^0 = the IC on the current mesh (snapshot 0) and eta = 0."""
     amp, freq, phase = self.ic
-    self.op.init_sine([amp], [freq], [phase], out=snaps[0])
+    self.op.init_sine([amp], [freq], [phase], out=self.snapshots()[0])
+    self.eta().zero_()
+
+  def forward(self, dt=None, init=True):
+    """init_state() (unless init=False: the caller did it) then the forward sweep."""
+    snaps = self.snapshots()
+    if init:
+      self.init_state()
     self.op.forward(snaps[0], self.t0, self.dt if dt is None else dt, self.nsteps, snaps)
     return snaps
 
   def adjoint(self, dt=None):
+    """The adjoint sweep accumulating into eta (zeroed by init_state)."""
     snaps = self.snapshots()
     eta = self.eta()
-    eta.zero_()
     # J = |u^N|^2 / 2: the terminal adjoint is u^N itself; the sweep runs in place on it.
     self.op.adjoint(snaps[self.nsteps], snaps, self.t0, self.dt if dt is None else dt,
                     self.nsteps, eta=eta)

@@ -730,8 +730,13 @@ int launch_nl_step(const dg_plan* p, int ms, const double* in, double* snap, dou
 }
 
 // Steps per launch of the limited kernels: 1 or 2 (the cone is 10 elements per step).
-inline int chunk_nl(const dg_plan* p, int left) {
-  const int m = p->msteps >= 2 ? 2 : 1;
+// Steps per limited-forward launch.  The kernels are VALU-bound, so the 2-step cone's
+// extra halo (20 instead of 10 elements per 256-element tile) costs more than the HBM
+// round trip it saves whenever the snapshots are written anyway: the default (msteps 4)
+// runs 1 step per launch with snapshots and 2 without (A/B at K = 2^22: 82 against 88 µs
+// per step with snapshots, 84 against 80.5 without).  An explicit msteps of 1 or 2 is kept.
+inline int chunk_nl(const dg_plan* p, int left, bool snapshots) {
+  const int m = (p->msteps == 2 || (p->msteps > 2 && !snapshots)) ? 2 : 1;
   return m > left ? left : m;
 }
 
@@ -760,7 +765,7 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
     if (snapshots != u)
       HIP_TRY(hipMemcpyAsync(snapshots, u, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
     for (int n = 0; n < nsteps;) {
-      const int m = chunk_nl(p, nsteps - n);
+      const int m = chunk_nl(p, nsteps - n, true);
       double* last = (n + m == nsteps && snapshots != u) ? u : nullptr;
       const int rc = launch_nl_step(p, m, snapshots + int64_t(n) * field,
                                     snapshots + int64_t(n + 1) * field, last, &tn[n], dt, st);
@@ -770,7 +775,7 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
     return DG_OK;
   }
   int launches = 0;  // ping-pong u <-> scratch, landing the last launch in u
-  for (int n = 0; n < nsteps; n += chunk_nl(p, nsteps - n)) ++launches;
+  for (int n = 0; n < nsteps; n += chunk_nl(p, nsteps - n, false)) ++launches;
   double* a = u;
   double* b = p->d_scratch;
   if (launches % 2 == 1) {
@@ -778,7 +783,7 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
     std::swap(a, b);
   }
   for (int n = 0; n < nsteps;) {
-    const int m = chunk_nl(p, nsteps - n);
+    const int m = chunk_nl(p, nsteps - n, false);
     const int rc = launch_nl_step(p, m, a, nullptr, b, &tn[n], dt, st);
     if (rc) return rc;
     std::swap(a, b);
