@@ -103,7 +103,7 @@ int dg_plan_tune(dg_plan* plan, int key, int64_t value);
  *   DG_LIMIT_PI1_EACH_STAGE  u = SlopeLimit1(u) (utils/SlopeLimit1.m:1-23, every cell limited)
  *                       after every stage update
  * Both need DG_TIME_LSERK4.  With either, dg_advec_rhs evaluates the flux's RHS (no limiter),
- * dg_lserk4_fwd runs limited steps (at most 2 per launch), and dg_lserk4_adj is the exact
+ * dg_lserk4_fwd runs limited steps (1 or 2 per launch), and dg_lserk4_adj is the exact
  * transpose of each step's tangent at the stored forward states, with the limiter's discrete
  * decisions (troubled cells, active minmod argument) frozen; it recomputes step n's stages from
  * snapshots[n] (one launch per step) and takes the indicator residual of the flux f. */
