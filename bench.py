@@ -291,6 +291,7 @@ def main():
   t0 = time.perf_counter()
   for s in range(args.steps):
     one_step(evs[s])
+  host_issue = time.perf_counter() - t0  # host time to enqueue the steps (launch-bound check)
   torch.cuda.synchronize()
   ref_idx = int(idx_host.item())
   pkg.adaptive.check_indicator(float(val_host.item()), ref_idx)
@@ -390,6 +391,7 @@ def main():
                       "adj_frac_of_achievable": adj_gbs / copy_gbs if copy_gbs else None},
       "steps_per_launch": ms,
       "refine_index": ref_idx,
+      "host_issue_ms_per_step": host_issue / args.steps * 1e3,
   }
   if rank == 0 and world == 1 and args.ics == 0 and not args.no_cpu_baseline:
     out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_steps)
