@@ -57,6 +57,7 @@ class AdaptiveSweep:
     # min |x_1 - x_2| over elements = h_min * (r_1 - r_0) / 2 (LGL nodes are affine images)
     self._half_gap = 0.5 * float(mesh.r_gl[1] - mesh.r_gl[0])
     self.h_min = float(np.min(np.diff(mesh.v_x)))
+    self._length = float(np.max(np.abs(mesh.v_x)))
     self.history = []
 
   @property
@@ -113,7 +114,11 @@ class AdaptiveSweep:
     """Bring the refine index and the split width to the host; update h_min."""
     idx = int(self.idx.item())
     check_indicator(float(self._eta_at.item()), idx)
-    self.h_min = min(self.h_min, 0.5 * float(self.h_split.item()))
+    h_new = 0.5 * float(self.h_split.item())
+    if not h_new > 64 * np.finfo(np.float64).eps * self._length:
+      raise FloatingPointError(f"refining element {idx} left elements of width {h_new:g}: "
+                               "the split has reached fp64 resolution of the coordinates")
+    self.h_min = min(self.h_min, h_new)
     self.history.append(idx)
     return idx
 

@@ -35,8 +35,11 @@ PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 def parse():
   p = argparse.ArgumentParser()
   p.add_argument("--gpus", type=int, default=1)
-  p.add_argument("--steps", type=int, default=10)
-  p.add_argument("--warmup", type=int, default=3)
+  p.add_argument("--steps", type=int, default=None,
+                 help="timed steps (default 100; config 3: 10 refine iterations)")
+  p.add_argument("--warmup", type=int, default=None,
+                 help="untimed steps first (default 50, which also lets the GPU clocks settle; "
+                      "config 3: 3)")
   p.add_argument("--N", type=int, default=4)
   p.add_argument("--config", type=int, default=2, choices=(2, 3),
                  help="2: linear advection (headline); 3: Burgers flux + limiter refine loop")
@@ -50,7 +53,14 @@ def parse():
   p.add_argument("--graph", action="store_true",
                  help="replay each sweep as a captured HIP graph (measured 1-3%% slower than "
                       "eager launches on this path, profiles/r01/bench_eager_vs_graph.txt)")
-  return p.parse_args()
+  a = p.parse_args()
+  # Config 3 refines one element per step, so its step count is bounded by how often the
+  # loop can split the same region before the element width reaches fp64 resolution.
+  if a.steps is None:
+    a.steps = 10 if a.config == 3 else 100
+  if a.warmup is None:
+    a.warmup = 3 if a.config == 3 else 50
+  return a
 
 
 def stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
