@@ -39,7 +39,7 @@ def parse():
                  help="timed steps (default 100; config 3: 10 refine iterations)")
   p.add_argument("--warmup", type=int, default=None,
                  help="untimed steps first (default 50, which also lets the GPU clocks settle; "
-                      "config 3: 3)")
+                      "config 3: 8)")
   p.add_argument("--N", type=int, default=4)
   p.add_argument("--config", type=int, default=2, choices=(2, 3),
                  help="2: linear advection (headline); 3: Burgers flux + limiter refine loop")
@@ -59,7 +59,7 @@ def parse():
   if a.steps is None:
     a.steps = 10 if a.config == 3 else 100
   if a.warmup is None:
-    a.warmup = 3 if a.config == 3 else 50
+    a.warmup = 8 if a.config == 3 else 50
   return a
 
 
