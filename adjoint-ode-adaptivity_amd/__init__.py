@@ -15,17 +15,19 @@ Submodules:
   dgtime     batched DG-in-time marches + DWR for ODE ensembles (matlab/MAIN.m loop)
   fd_ensemble  the finite-difference DWR adapt loop for ODE ensembles on the device
   globals_io Save_to_1D_global_data.m-compatible operator/mesh dumps
+  checkpoint CheckpointedSweep: adjoint sweeps from every m-th state (recompute in between)
   build_ext  in-tree hipcc build of lib/libdgadv.so
 """
 from . import _lib, galerkin  # noqa: F401
 from .galerkin import BaseGalerkin1D, split_interval  # noqa: F401
 
-__all__ = ["BaseGalerkin1D", "split_interval", "operators", "factory", "ensemble", "adaptive", "dgtime", "fd_ensemble", "globals_io", "galerkin"]
+__all__ = ["BaseGalerkin1D", "split_interval", "operators", "factory", "ensemble", "adaptive", "dgtime", "fd_ensemble", "globals_io", "galerkin", "checkpoint"]
 
 
 def __getattr__(name):
   # torch-dependent modules load on first use (the host setup does not need torch).
-  if name in ("operators", "factory", "ensemble", "adaptive", "dgtime", "fd_ensemble", "globals_io"):
+  if name in ("operators", "factory", "ensemble", "adaptive", "dgtime", "fd_ensemble", "globals_io",
+              "checkpoint"):
     import importlib
     return importlib.import_module(f"{__name__}.{name}")
   if name == "DGAdvection1D":
