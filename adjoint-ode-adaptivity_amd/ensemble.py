@@ -117,6 +117,10 @@ class EnsembleSweep:
     self.adjoint()
     return self.reduce()
 
+  def per_ic(self):
+    """This rank's per-IC indicators, (batch, K) — a view of eta (IC b is row b)."""
+    return self.eta.view(self.batch, self.op.K)
+
 
 class DeviceReducer:
   """Fixed-order sum and numpy-semantics argmax through the HIP library."""
@@ -162,3 +166,30 @@ def gather_indicator(partial, n_total, reducer, group=None):
   # dividing by 1 is exact (bit-identical shortcut)
   mean = total / float(n_total) if n_total != 1 else total
   return mean, reducer.argmax(mean)
+
+
+def gather_per_ic(rows, n_total, group=None):
+  """All-gather every rank's per-IC indicator rows (``rows``: (batch_r, K), the ICs
+  ``shard(n_total, rank, W)``) into the (n_total, K) array of all ICs in IC order, on every
+  rank — the per-IC training-data gather of north_star (Main_width_ref.py:466-478 computes
+  one indicator row per IC; models.py trains on them).
+
+  Shards differ by at most one IC, so each rank pads its block to ceil(n_total/W) rows and
+  one all_gather_into_tensor (RCCL over xGMI on GPUs) moves W * ceil(n_total/W) * K doubles
+  (512 MiB at config 4); the pad rows are dropped.  Pure data movement: the result is
+  bit-identical to the rows."""
+  if dist.is_available() and dist.is_initialized():
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+  else:
+    world, rank = 1, 0
+  rows = rows.reshape(len(shard(n_total, rank, world)), -1)
+  if world == 1:
+    return rows
+  K = rows.shape[1]
+  per = -(-n_total // world)
+  send = rows.new_zeros(per, K)
+  send[: rows.shape[0]] = rows
+  full = rows.new_empty(world * per, K)
+  dist.all_gather_into_tensor(full, send, group=group)
+  keep = [r * per + i for r in range(world) for i in range(len(shard(n_total, r, world)))]
+  return full[torch.tensor(keep, device=full.device)]

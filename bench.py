@@ -45,6 +45,9 @@ def parse():
                  help="2: linear advection (headline); 3: Burgers flux + limiter refine loop")
   p.add_argument("--K", type=int, default=None, help="elements (default 2^20; config 3: 2^22)")
   p.add_argument("--nsteps", type=int, default=20, help="time steps per sweep (each direction)")
+  p.add_argument("--gather-ics", action="store_true",
+                 help="also all-gather every IC's indicator row to every rank each step "
+                      "(the per-IC training-data path; 512 MiB at config 4)")
   p.add_argument("--ics", type=int, default=0,
                  help="ensemble size over all ranks (config 4: --K 65536 --ics 1024); "
                       "default: one trajectory per rank (config 2 per GPU, weak scaling)")
@@ -284,6 +287,8 @@ def main():
       ev[3].record(stream)
     partial = sweep.reduce()
     mean, idx = ens.gather_indicator(partial, n_total, reducer)
+    if args.gather_ics:
+      ens.gather_per_ic(sweep.per_ic(), n_total)
     # The refine index goes to the host (the mesh split's input) without stalling the
     # stream: an async copy into pinned memory, read once the timed region has synced.
     # The indicator there is finite iff it is finite everywhere (argmax ranks NaN first).
@@ -379,7 +384,8 @@ def main():
                               f"K={K} x {n_total} trajectories, LSERK4 fwd+adj {nsteps}+{nsteps} "
                               f"steps/sweep + DWR indicator + refine argmax"),
                  "N": N, "K": K, "nsteps_per_sweep": nsteps, "trajectories": n_total,
-                 "trajectories_per_gpu": sweep.batch, "parallelism": f"ensemble-dp{world}"},
+                 "trajectories_per_gpu": sweep.batch, "parallelism": f"ensemble-dp{world}",
+                 "per_ic_gather": bool(args.gather_ics)},
       "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
                    "kernel": f"k_adj<{Np},5,uniform,{sweep.op.tile_width},{ms}> ({ms} reverse steps + DWR per launch)",

@@ -451,3 +451,25 @@ def test_dg_adapt_loop_refines_the_oracle_argmax(pkg, gpu):
     assert len(state.times_new) == len(v_x_now) + 1
     seen.append(state.ref_idx)
   assert len(state.times_new) == 45  # four splits of a 40-element mesh
+
+
+def test_ensemble_per_ic_rows_and_gather(pkg, gpu):
+  """per_ic() rows are each IC's own indicator; their fixed-order sum is reduce(); the
+  single-process per-IC gather returns them unchanged."""
+  import torch
+  K, ics = 200, [3, 4, 5]
+  mesh = pkg.BaseGalerkin1D(n=4, k=K)
+  S = setup1d.uniform_setup(4, K, metric="element")
+  dt = oadv.bench_dt(S)
+  sweep = pkg.ensemble.EnsembleSweep(mesh, ics, 8, dt)
+  partial = sweep.run().clone()
+  rows = sweep.per_ic()
+  assert rows.shape == (3, K)
+  torch.testing.assert_close(pkg.operators.sum_rows(rows.contiguous(), 3), partial, rtol=0,
+                             atol=0)
+  for b, j in enumerate(ics):
+    one = pkg.ensemble.EnsembleSweep(mesh, [j], 8, dt)
+    one.run()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(rows[b]), host(one.eta))
+  assert torch.equal(pkg.ensemble.gather_per_ic(rows, 3), rows)
