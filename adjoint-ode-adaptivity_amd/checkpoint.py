@@ -89,6 +89,9 @@ class CheckpointedSweep:
     full snapshot array.  w must not alias the scratch."""
     if self._times is None:
       raise RuntimeError("adjoint() needs a preceding forward()")
+    lo, hi = self.scratch.data_ptr(), self.scratch.data_ptr() + self.scratch.nbytes
+    if lo <= w.data_ptr() < hi:
+      raise ValueError("w must not alias the scratch (copy the terminal state first)")
     for c in range(len(self.segments) - 1, -1, -1):
       s, e = self.segments[c]
       snaps = self.scratch[: e - s + 1]

@@ -120,3 +120,11 @@ def test_adjoint_needs_forward():
     sweep.adjoint(torch.zeros(7, dtype=torch.float64))
   with pytest.raises(ValueError):
     ck.CheckpointedSweep(LinearStandIn(), 0)
+
+
+def test_adjoint_refuses_w_in_the_scratch():
+  op = LinearStandIn()
+  sweep = ck.CheckpointedSweep(op, 4, 2)
+  sweep.forward(torch.ones(op.F, dtype=torch.float64), 0.0, 0.1)
+  with pytest.raises(ValueError):
+    sweep.adjoint(sweep.scratch[2])
