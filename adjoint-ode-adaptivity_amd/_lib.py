@@ -19,6 +19,7 @@ DG_TUNE_TILE_WIDTH, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
 DG_TUNE_LANE_ELEMENTS = 4
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
+DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
 
 _c_dbl_p = ctypes.POINTER(ctypes.c_double)
 _vp = ctypes.c_void_p
@@ -42,9 +43,13 @@ SIGNATURES = {
     "dg_lserk4_fwd": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp]),
     "dg_lserk4_adj": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32,
                              ctypes.c_double, _vp, _vp]),
+    "dg_lserk4_adj_ex": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32,
+                                ctypes.c_double, _vp, _i32, _vp]),
     "dg_slope_limit_n": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dg_slope_limit_1": (_i32, [_vp, _vp, _vp, _vp]),
     "dg_argmax": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
+    "dg_argmax_ex": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "dg_stream_copy": (_i32, [_vp, _vp, _i64, _vp]),
     "dg_sum_rows": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "dg_init_sine": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "dg_time_march": (_i32, [_i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp, ctypes.c_double,

@@ -31,6 +31,19 @@ int fail(int code, const std::string& msg) {
 namespace {
 using namespace dgk;
 
+template <int NP, int NS, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_step(const double* __restrict__ uin,
+                                                     double* __restrict__ snap,
+                                                     double* __restrict__ last,
+                                                     const double* __restrict__ scale,
+                                                     StepArgs<NP, NS, MS> args);
+template <int NP, int NS, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_adj(const double* __restrict__ win,
+                                                    double* __restrict__ wout,
+                                                    const double* __restrict__ snap,
+                                                    double* __restrict__ eta,
+                                                    const double* __restrict__ scale,
+                                                    AdjArgs<NP, MS> args);
 
 // ---------------------------------------------------------------------------
 // Forward fused kernel: MS time steps of NS stages (AdvecRHS1D + the low-storage update)
@@ -63,12 +76,12 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
   tile_commit<NP, W>(pf, lds);
   if constexpr (EDGE) {
     // Lane-indexed read straight from the kernel-argument segment (k_step's args follow
-    // its 4 pointer arguments): read as a uniform struct member, the compiler hoists these
-    // 2*MS*NS SGPRs over the whole kernel and pushes the interior path into SGPR spills.
+    // its pointer arguments; layout pinned by kernarg_tail): read as a uniform struct member,
+    // the compiler hoists these 2*MS*NS SGPRs over the whole kernel and pushes the interior
+    // path into SGPR spills.
     using SArgs = StepArgs<NP, NS, MS>;
     const double* ka = reinterpret_cast<const double*>(
-        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 4 * sizeof(void*) +
-        offsetof(SArgs, uin));
+        kernarg_tail<decltype(&k_step<NP, NS, UNI, W, MS>), SArgs>() + offsetof(SArgs, uin));
     if (lane < MS * NS) lds[CB + lane] = ka[lane];
   }
   __syncthreads();
@@ -231,9 +244,8 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
   tile_commit<NP, W>(pw, lds);
   if constexpr (EDGE) {
     using AArgs = AdjArgs<NP, MS>;
-    const double* ka = reinterpret_cast<const double*>(  // see step_tile; 5 pointer args
-        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 5 * sizeof(void*) +
-        offsetof(AArgs, uin_res));
+    const double* ka = reinterpret_cast<const double*>(  // see step_tile
+        kernarg_tail<decltype(&k_adj<NP, NS, UNI, W, MS>), AArgs>() + offsetof(AArgs, uin_res));
     if (lane < MS) lds[CB + lane] = ka[lane];
     if (lane == MS) lds[CB + MS] = 0.0;
   }
@@ -389,7 +401,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 
 #pragma unroll
   for (int m = 0; m < EPL; ++m)
-    if (args.has_eta && E[m].valid) eta[E[m].e] += eacc[m];
+    if (args.has_eta && E[m].valid) eta_update(eta, E[m].e, eacc[m], args.has_eta);
   stage_out<NP, W, H>(lds, we, wo, true);  // the image's last reads are 5 barriers behind
   __syncthreads();
   const int64_t o0 = tile * TE * NP;
@@ -634,6 +646,31 @@ __global__ __launch_bounds__(kBlock) void k_argmax_final(const double* __restric
   if (threadIdx.x == 0) out[0] = bi;
 }
 
+// dg_argmax_ex: as k_argmax_final, and also hands back the winning value (|x| when use_abs)
+// and counts a non-finite winner.  argmax ranks NaN first and +inf above every finite value,
+// so the winner is non-finite exactly when some entry is NaN or +-inf (under use_abs; without
+// it a -inf elsewhere is not seen).  One thread writes, in stream order: no atomics needed.
+__global__ __launch_bounds__(kBlock) void k_argmax_final_ex(const double* __restrict__ pv,
+                                                            const int64_t* __restrict__ pi,
+                                                            int nparts, int64_t* __restrict__ out,
+                                                            double* __restrict__ val,
+                                                            int64_t* __restrict__ nonfinite) {
+  double bv = -INFINITY;
+  int64_t bi = INT64_MAX;
+  for (int p = threadIdx.x; p < nparts; p += kBlock) {
+    if (better(pv[p], pi[p], bv, bi)) {
+      bv = pv[p];
+      bi = pi[p];
+    }
+  }
+  block_argmax(bv, bi);
+  if (threadIdx.x == 0) {
+    out[0] = bi;
+    if (val != nullptr) val[0] = bv;
+    if (nonfinite != nullptr && !isfinite(bv)) nonfinite[0] += 1;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_sum_rows(const double* __restrict__ x, int64_t rows,
                                                      int64_t n, double* __restrict__ out) {
   const int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x;
@@ -742,7 +779,7 @@ int launch_step_e(const dg_plan* p, const double* in, double* snap, double* last
 
 template <int NP, int NS, int W, int MS>
 int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double* snap,
-                 double* eta, const double* t_next, const double* src, double dt,
+                 double* eta, int eta_mode, const double* t_next, const double* src, double dt,
                  hipStream_t st) {
   AdjArgs<NP, MS> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
@@ -754,7 +791,7 @@ int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double
   a.ktot = p->ktot;
   a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
-  a.has_eta = eta != nullptr;
+  a.has_eta = eta != nullptr ? (eta_mode | kEtaOn) : 0;
   a.xcd = p->xcd_order;
   constexpr int TE = kBlock * W - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
@@ -789,21 +826,23 @@ int launch_step_t(const dg_plan* p, int ms, const double* in, double* snap, doub
 
 template <int NP, int NS>
 int launch_adj_t(const dg_plan* p, int ms, const double* win, double* wout, const double* snap,
-                 double* eta, const double* t_next, const double* src, double dt,
+                 double* eta, int em, const double* t_next, const double* src, double dt,
                  hipStream_t st) {
   const bool w2 = p->tile_width == 2;
   if constexpr (NP <= 8) {
     if (ms == 8)
-      return launch_adj_e<NP, NS, 2, 8>(p, win, wout, snap, eta, t_next, src, dt, st);
+      return launch_adj_e<NP, NS, 2, 8>(p, win, wout, snap, eta, em, t_next, src, dt, st);
     if (ms == 4 && w2)
-      return launch_adj_e<NP, NS, 2, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
-    if (ms == 4) return launch_adj_e<NP, NS, 1, 4>(p, win, wout, snap, eta, t_next, src, dt, st);
+      return launch_adj_e<NP, NS, 2, 4>(p, win, wout, snap, eta, em, t_next, src, dt, st);
+    if (ms == 4)
+      return launch_adj_e<NP, NS, 1, 4>(p, win, wout, snap, eta, em, t_next, src, dt, st);
   }
   if (ms == 2 && w2)
-    return launch_adj_e<NP, NS, 2, 2>(p, win, wout, snap, eta, t_next, src, dt, st);
-  if (ms == 2) return launch_adj_e<NP, NS, 1, 2>(p, win, wout, snap, eta, t_next, src, dt, st);
-  if (w2) return launch_adj_e<NP, NS, 2, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
-  return launch_adj_e<NP, NS, 1, 1>(p, win, wout, snap, eta, t_next, src, dt, st);
+    return launch_adj_e<NP, NS, 2, 2>(p, win, wout, snap, eta, em, t_next, src, dt, st);
+  if (ms == 2)
+    return launch_adj_e<NP, NS, 1, 2>(p, win, wout, snap, eta, em, t_next, src, dt, st);
+  if (w2) return launch_adj_e<NP, NS, 2, 1>(p, win, wout, snap, eta, em, t_next, src, dt, st);
+  return launch_adj_e<NP, NS, 1, 1>(p, win, wout, snap, eta, em, t_next, src, dt, st);
 }
 
 int launch_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
@@ -820,14 +859,15 @@ int launch_step(const dg_plan* p, int ms, const double* in, double* snap, double
 }
 
 int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const double* snap,
-               double* eta, const double* t_next, const double* src, double dt, hipStream_t st) {
+               double* eta, int em, const double* t_next, const double* src, double dt,
+               hipStream_t st) {
   int rc = DG_OK;
   if (p->nstages == 5) {
-    DG_DISPATCH_NP(p->NP,
-                   rc = (launch_adj_t<NP, 5>(p, ms, win, wout, snap, eta, t_next, src, dt, st)));
+    DG_DISPATCH_NP(p->NP, rc = (launch_adj_t<NP, 5>(p, ms, win, wout, snap, eta, em, t_next, src,
+                                                    dt, st)));
   } else {
-    DG_DISPATCH_NP(p->NP,
-                   rc = (launch_adj_t<NP, 1>(p, ms, win, wout, snap, eta, t_next, src, dt, st)));
+    DG_DISPATCH_NP(p->NP, rc = (launch_adj_t<NP, 1>(p, ms, win, wout, snap, eta, em, t_next, src,
+                                                    dt, st)));
   }
   return rc;
 }
@@ -1155,10 +1195,18 @@ int dg_lserk4_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, doubl
 
 int dg_lserk4_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
                   int nsteps, double src_coef, double* eta, void* stream) {
+  return dg_lserk4_adj_ex(p, w, snapshots, t0, dt, nsteps, src_coef, eta, 0, stream);
+}
+
+int dg_lserk4_adj_ex(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
+                     int nsteps, double src_coef, double* eta, int flags, void* stream) {
   if (!p || !w || !snapshots) return fail(DG_ERR_ARG, "null argument");
   if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
+  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS)) return fail(DG_ERR_ARG, "unknown flags");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (p->nonlinear()) return nl_adj(p, w, snapshots, t0, dt, nsteps, src_coef, eta, st);
+  if (eta != nullptr && nsteps == 0 && (flags & DG_ADJ_ETA_ASSIGN))  // nothing to assign from
+    HIP_TRY(hipMemsetAsync(eta, 0, sizeof(double) * p->ktot, st));
+  if (p->nonlinear()) return nl_adj(p, w, snapshots, t0, dt, nsteps, src_coef, eta, flags, st);
   const int64_t field = p->ktot * p->NP;
   // Same time levels as the forward sweep (repeated addition).
   std::vector<double> tn(size_t(nsteps) + 1), src(size_t(nsteps) + 1, src_coef);
@@ -1178,7 +1226,11 @@ int dg_lserk4_adj(dg_plan* p, double* w, const double* snapshots, double t0, dou
     // (a single launch cannot write its own input: it goes through scratch and back)
     double* out = (l == launches - 1 && launches > 1)
                       ? w : ((l % 2 == 0) ? p->d_scratch : p->d_scratch2);
-    const int rc = launch_adj(p, m, in, out, snapshots + int64_t(n0 + 1) * field, eta,
+    // DG_ADJ_ETA_ASSIGN: the sweep's first launch assigns eta; DG_ADJ_ETA_ABS: its last
+    // launch stores |eta|.
+    const int em = ((l == 0 && (flags & DG_ADJ_ETA_ASSIGN)) ? kEtaAssign : 0) |
+                   ((n0 == 0 && (flags & DG_ADJ_ETA_ABS)) ? kEtaAbs : 0);
+    const int rc = launch_adj(p, m, in, out, snapshots + int64_t(n0 + 1) * field, eta, em,
                               &tn[n0 + 1], &src[n0 + 1], dt, st);
     if (rc) return rc;
     in = out;
@@ -1226,6 +1278,22 @@ int dg_argmax(dg_plan* p, const double* x, int64_t n, int use_abs, int64_t* idx,
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(kBlock), 0, st, p->d_pv, p->d_pi, int(parts),
                      idx);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+int dg_argmax_ex(dg_plan* p, const double* x, int64_t n, int use_abs, int64_t* idx,
+                 double* value, int64_t* nonfinite_count, void* stream) {
+  if (!p || !x || !idx) return fail(DG_ERR_ARG, "null argument");
+  if (n < 1 || n > p->ktot * p->NP) return fail(DG_ERR_ARG, "n out of range");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t parts = (n + 4 * kBlock - 1) / (4 * kBlock);
+  if (parts > kArgmaxParts) parts = kArgmaxParts;
+  hipLaunchKernelGGL(k_argmax_partial, dim3(unsigned(parts)), dim3(kBlock), 0, st, x, n, use_abs,
+                     p->d_pv, p->d_pi);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_argmax_final_ex, dim3(1), dim3(kBlock), 0, st, p->d_pv, p->d_pi,
+                     int(parts), idx, value, nonfinite_count);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }

@@ -227,6 +227,13 @@ template <int NP, int MS> struct NLStepArgs {
 
 template <bool LIM> constexpr int cone_per_stage() { return LIM ? 2 : 1; }
 
+template <int NP, bool BURG, bool LIM, bool UNI, int MS>
+__global__ __launch_bounds__(kBlock) void k_step_nl(const double* __restrict__ uin,
+                                                    double* __restrict__ snap,
+                                                    double* __restrict__ last,
+                                                    const double* __restrict__ scale,
+                                                    NLStepArgs<NP, MS> args);
+
 template <int NP, bool BURG, bool LIM, bool UNI, int MS, bool EDGE>
 __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t tile,
                                              const double* __restrict__ uin,
@@ -250,10 +257,10 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
   tile_commit<NP, 1>(pf, lds);
   if constexpr (EDGE) {
     // Lane-indexed read of fin straight from the kernel-argument segment (the args follow
-    // the 4 pointer arguments of k_step_nl), as in k_step.
+    // the pointer arguments of k_step_nl; layout pinned by kernarg_tail), as in k_step.
     using SArgs = NLStepArgs<NP, MS>;
     const double* ka = reinterpret_cast<const double*>(
-        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 4 * sizeof(void*) +
+        kernarg_tail<decltype(&k_step_nl<NP, BURG, LIM, UNI, MS>), SArgs>() +
         offsetof(SArgs, fin));
     if (lane < MS * 5) lds[CB + lane] = ka[lane];
   }
@@ -315,9 +322,17 @@ template <int NP> struct NLAdjArgs {
   double src;      // functional source coefficient of node n+1
   int64_t ktot;
   int32_t K;
-  int32_t has_eta;
+  int32_t has_eta;  // kEta* bits
   int32_t xcd;
 };
+
+template <int NP, bool BURG, bool LIM, bool UNI>
+__global__ __launch_bounds__(kBlock) void k_adj_nl(const double* __restrict__ win,
+                                                   double* __restrict__ wout,
+                                                   const double* __restrict__ snap,
+                                                   double* __restrict__ eta,
+                                                   const double* __restrict__ scale,
+                                                   NLAdjArgs<NP> args);
 
 template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE>
 __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t tile,
@@ -343,10 +358,9 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   tile_issue<NP, 1, EDGE>(win, e0, nd, pw);
   tile_commit<NP, 1>(pu, lds);
   if constexpr (EDGE) {
-    using AArgs = NLAdjArgs<NP>;  // the args follow the 5 pointer arguments of k_adj_nl
+    using AArgs = NLAdjArgs<NP>;  // the args follow the pointer arguments of k_adj_nl
     const double* ka = reinterpret_cast<const double*>(
-        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 5 * sizeof(void*) +
-        offsetof(AArgs, fin));
+        kernarg_tail<decltype(&k_adj_nl<NP, BURG, LIM, UNI>), AArgs>() + offsetof(AArgs, fin));
     if (lane < 6) lds[CB + lane] = ka[lane];
     if (lane == 6) lds[CB + 6] = 0.0;
   }
@@ -536,7 +550,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     }
   }
 
-  if (args.has_eta && E.valid) eta[E.e] += eacc;
+  if (args.has_eta && E.valid) eta_update(eta, E.e, eacc, args.has_eta);
   __syncthreads();  // the last stage's face reads are done before the image is rewritten
   put_interior<NP, H>(lds, we, wo, true);
   __syncthreads();
@@ -673,7 +687,7 @@ int launch_step_nl(const dg_plan* p, const double* in, double* snap, double* las
 
 template <int NP, bool BURG, bool LIM>
 int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const double* snap,
-                  double* eta, double t_n, double src, double dt, hipStream_t st) {
+                  double* eta, int em, double t_n, double src, double dt, hipStream_t st) {
   NLAdjArgs<NP> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
   a.lc = make_lim_eo<NP>(p);
@@ -683,7 +697,7 @@ int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const doubl
   a.src = src;
   a.ktot = p->ktot;
   a.K = int32_t(p->K);
-  a.has_eta = eta != nullptr;
+  a.has_eta = eta != nullptr ? (em | kEtaOn) : 0;
   a.xcd = p->xcd_order;
   constexpr int TE = kBlock - 20 * cone_per_stage<LIM>();
   const unsigned grid = grid_for(p->ktot, TE);
@@ -715,11 +729,12 @@ int step_np(const dg_plan* p, int ms, const double* in, double* snap, double* la
 
 template <int NP>
 int adj_np(const dg_plan* p, const double* win, double* wout, const double* snap, double* eta,
-           double t_n, double src, double dt, hipStream_t st) {
+           int em, double t_n, double src, double dt, hipStream_t st) {
   const bool burg = p->flux == DG_FLUX_BURGERS, lim = p->limiter != 0;
-  if (burg && lim) return launch_adj_nl<NP, true, true>(p, win, wout, snap, eta, t_n, src, dt, st);
-  if (burg) return launch_adj_nl<NP, true, false>(p, win, wout, snap, eta, t_n, src, dt, st);
-  return launch_adj_nl<NP, false, true>(p, win, wout, snap, eta, t_n, src, dt, st);
+  if (burg && lim)
+    return launch_adj_nl<NP, true, true>(p, win, wout, snap, eta, em, t_n, src, dt, st);
+  if (burg) return launch_adj_nl<NP, true, false>(p, win, wout, snap, eta, em, t_n, src, dt, st);
+  return launch_adj_nl<NP, false, true>(p, win, wout, snap, eta, em, t_n, src, dt, st);
 }
 
 int launch_nl_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
@@ -793,7 +808,7 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
 }
 
 int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,
-           double src_coef, double* eta, hipStream_t st) {
+           double src_coef, double* eta, int flags, hipStream_t st) {
   const int64_t field = p->ktot * p->NP;
   std::vector<double> tn(size_t(nsteps) + 1);
   tn[0] = t0;
@@ -806,9 +821,12 @@ int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
   for (int n = nsteps - 1; n >= 0; --n, ++l) {
     double* out = (n == 0 && nsteps > 1) ? w : ((l % 2 == 0) ? p->d_scratch : p->d_scratch2);
     const double src = (n + 1 == nsteps) ? 0.0 : src_coef;  // left-endpoint rule
+    // DG_ADJ_ETA_ASSIGN / DG_ADJ_ETA_ABS: first launch assigns eta, last one stores |eta|
+    const int em = ((l == 0 && (flags & DG_ADJ_ETA_ASSIGN)) ? kEtaAssign : 0) |
+                   ((n == 0 && (flags & DG_ADJ_ETA_ABS)) ? kEtaAbs : 0);
     int rc = DG_OK;
-    DG_DISPATCH_NP(p->NP, rc = adj_np<NP>(p, in, out, snapshots + int64_t(n) * field, eta, tn[n],
-                                          src, dt, st));
+    DG_DISPATCH_NP(p->NP, rc = adj_np<NP>(p, in, out, snapshots + int64_t(n) * field, eta, em,
+                                          tn[n], src, dt, st));
     if (rc) return rc;
     in = out;
   }

@@ -12,6 +12,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <tuple>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -22,6 +24,44 @@ namespace dgk {
 constexpr int kBlock = 256;       // lanes per workgroup = elements per tile (incl. halo)
 constexpr int kMaxNP = 9;         // N <= 8
 constexpr int kArgmaxParts = 1024;
+
+// Indicator write mode of the adjoint kernels (the `has_eta` argument field):
+// bit 0 an indicator is wanted; bit 1 this launch assigns eta instead of adding to it (the
+// sweep's first launch under DG_ADJ_ETA_ASSIGN: no zero fill); bit 2 this launch stores
+// |eta| (the sweep's last launch under DG_ADJ_ETA_ABS).
+constexpr int kEtaOn = 1, kEtaAssign = 2, kEtaAbs = 4;
+
+__device__ __forceinline__ void eta_update(double* __restrict__ eta, int64_t e, double acc,
+                                           int mode) {
+  double v = (mode & kEtaAssign) ? acc : eta[e] + acc;
+  if (mode & kEtaAbs) v = fabs(v);
+  eta[e] = v;
+}
+
+// Kernel-argument layout pin for the edge tiles' lane-indexed kernarg reads.  A kernel whose
+// parameters are pointers followed by ONE trailing by-value argument struct A has A at byte
+// offset (#pointers)*8 of the kernarg segment: pointers are 8-byte aligned and A's alignment
+// is 8, so no padding precedes it.  kernarg_tail<&kernel, A>() checks that shape on the
+// kernel's own type at compile time, so a change to a parameter's type, count or to A's
+// alignment breaks the build instead of reading garbage.
+template <class F> struct KernargLayout;
+template <class... P> struct KernargLayout<void (*)(P...)> {
+  static constexpr int kParams = int(sizeof...(P));
+  using Tail = std::tuple_element_t<sizeof...(P) - 1, std::tuple<P...>>;
+  static constexpr int kPointers = (0 + ... + int(std::is_pointer_v<P>));
+  static constexpr size_t kTailOffset = size_t(kParams - 1) * sizeof(void*);
+};
+
+template <class F, class A>
+__device__ __forceinline__ const char* kernarg_tail() {
+  using L = KernargLayout<F>;
+  static_assert(std::is_same_v<typename L::Tail, A>, "kernel's last parameter is not A");
+  static_assert(L::kPointers == L::kParams - 1, "all parameters before A must be pointers");
+  static_assert(sizeof(void*) == 8 && alignof(A) == 8, "A must follow 8-byte pointers unpadded");
+  static_assert(std::is_standard_layout_v<A> && std::is_trivially_copyable_v<A>,
+                "offsetof needs a standard-layout argument struct");
+  return (const char*)__builtin_amdgcn_kernarg_segment_ptr() + L::kTailOffset;
+}
 
 // Sets the calling thread's dg_last_error() text and returns `code` (dg_advec.hip).
 int fail(int code, const std::string& msg);
@@ -110,7 +150,7 @@ template <int NP, int MS> struct AdjArgs {
   int64_t ktot;
   int64_t stride;      // doubles between consecutive snapshots
   int32_t K;
-  int32_t has_eta;
+  int32_t has_eta;     // kEta* bits
   int32_t xcd;         // XCD-aware tile order (speed only)
 };
 
@@ -484,7 +524,7 @@ int nl_rhs(const dg_plan* p, const double* u, double* rhs, double t, hipStream_t
 int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
            hipStream_t st);
 int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,
-           double src_coef, double* eta, hipStream_t st);
+           double src_coef, double* eta, int flags, hipStream_t st);
 
 // Wave-tile variants of the linear LSERK4 step kernels (dg_wave.hip), selected by
 // plan->lane_elems; `times` as for the workgroup-tile launchers.

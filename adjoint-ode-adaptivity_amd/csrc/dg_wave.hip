@@ -40,6 +40,13 @@ template <int NP, int E, int MS, int NS> struct WaveGeo {
   static constexpr int kVec = (kTileD + 2 * LB - 1) / (2 * LB);  // double2 loads per lane
 };
 
+template <int NP, int NS, bool UNI, int E, int MS>
+__global__ __launch_bounds__(64) void k_wstep(const double* __restrict__ uin,
+                                              double* __restrict__ snap,
+                                              double* __restrict__ last,
+                                              const double* __restrict__ scale,
+                                              StepArgs<NP, NS, MS> args);
+
 template <int NP, int NS, bool UNI, int E, int MS, bool EDGE>
 __device__ __forceinline__ void wstep_tile(double* __restrict__ lds, int64_t tile,
                                            const double* __restrict__ uin,
@@ -89,8 +96,7 @@ __device__ __forceinline__ void wstep_tile(double* __restrict__ lds, int64_t til
     if constexpr (EDGE) {
       using SArgs = StepArgs<NP, NS, MS>;  // kernarg read of uin[], see step_tile
       const double* ka = reinterpret_cast<const double*>(
-          (const char*)__builtin_amdgcn_kernarg_segment_ptr() + 4 * sizeof(void*) +
-          offsetof(SArgs, uin));
+          kernarg_tail<decltype(&k_wstep<NP, NS, UNI, E, MS>), SArgs>() + offsetof(SArgs, uin));
       if (lane < MS * NS) lds[CB + lane] = ka[lane];
     }
     __syncthreads();

@@ -127,9 +127,12 @@ class DGTimeEnsemble:
     return V, err
 
   def indicator(self, err):
-    """Per-slab indicator summed over the ensemble in member order (dg_sum_rows)."""
+    """Per-slab indicator: sum over the ensemble, in member order (dg_sum_rows), of each
+    member's |err| -- MAIN.m:137 refines by |err| of its one trajectory, and the ensemble
+    path takes that magnitude per member before combining (Main_width_ref.py:139,479 and
+    FDEnsemble do the same), so opposite-signed members never cancel."""
     from .operators import sum_rows
-    return sum_rows(err.contiguous(), self.n_ics)
+    return sum_rows(err.abs().contiguous(), self.n_ics)
 
   def adapt(self):
     """One MAIN.m iteration: march, adjoint, indicator, split.  Returns the refined slab."""

@@ -4,7 +4,9 @@ The reference's only data-parallel axis is the ensemble of initial conditions
 (``vmap`` over ICs, python/Main_width_ref.py:466-478), reduced by a mean over ICs and
 an argmax (:479, :491).  Here each rank owns a contiguous block of ICs, runs the
 forward + adjoint sweeps for all of them as one batched plan (no data-path
-communication), reduces its per-IC indicators to one K-vector in fixed order, and the
+communication), takes each IC's indicator magnitude |eta_ic| (the reference's
+errorIndicator returns ``jnp.abs(err)`` per IC, :139, before the mean over ICs, :479),
+reduces them to one K-vector in fixed order, and the
 ranks sum those partial sums in rank order with a reduce-scatter built from one
 all-to-all (each rank owns a 1/W slice and adds the W partials of it in rank order)
 and one all-gather of the summed slices (RCCL over xGMI on GPUs).  The mean indicator
@@ -39,7 +41,10 @@ def shard(n_total, rank, world):
 
 class EnsembleSweep:
   """One forward + adjoint sweep over this rank's ICs, producing the rank's partial
-  indicator sum (K values).  J = 1/2 |u(T)|^2 per IC (terminal adjoint w^N = u^N).
+  indicator sum sum_ic |eta_ic| (K values).  J = 1/2 |u(T)|^2 per IC (terminal adjoint
+  w^N = u^N).  Each IC's row is stored as |eta_ic| by the last adjoint launch
+  (DG_ADJ_ETA_ABS), as python/Main_width_ref.py:139 returns jnp.abs(err) per IC, so
+  opposite-signed indicators of different ICs never cancel in the mean.
 
   All work is enqueued on torch's current stream; ``run`` does not synchronise.
   """
@@ -59,6 +64,8 @@ class EnsembleSweep:
     # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
     # place on snapshot N (the library allows that alias) and leaves dJ/du^0 there.
     self.w = self.snaps[self.nsteps]
+    # per-IC |eta| rows; the adjoint's first launch assigns them (DG_ADJ_ETA_ASSIGN), so
+    # they need no zero fill
     self.eta = torch.zeros(self.op.ktot, dtype=torch.float64, device=self.op.device)
     self.partial = torch.zeros(self.op.K, dtype=torch.float64, device=self.op.device)
     self._graphs = None
@@ -72,12 +79,13 @@ class EnsembleSweep:
     self.op.forward(self.snaps[0], 0.0, self.dt, self.nsteps, self.snaps)
 
   def adjoint(self):
-    self.eta.zero_()
     self.run_adjoint()
 
   def run_adjoint(self):
-    """The adjoint kernels alone (eta already zeroed by the caller)."""
-    self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta)
+    """The adjoint kernels: w^N -> w^0 in place and eta = |DWR| per IC row (assigned, not
+    accumulated: no zero fill needed)."""
+    self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta,
+                    eta_assign=True, eta_abs=True)
 
   def capture(self):
     """Capture the forward and adjoint sweeps as two HIP graphs (replayed by
@@ -118,21 +126,42 @@ class EnsembleSweep:
     return self.reduce()
 
   def per_ic(self):
-    """This rank's per-IC indicators, (batch, K) — a view of eta (IC b is row b)."""
+    """This rank's per-IC indicator magnitudes |eta_ic|, (batch, K) — a view of eta (IC b
+    is row b), the rows Main_width_ref.py:139 returns."""
     return self.eta.view(self.batch, self.op.K)
 
 
 class DeviceReducer:
-  """Fixed-order sum and numpy-semantics argmax through the HIP library."""
+  """Fixed-order sum and numpy-semantics argmax through the HIP library.
+
+  ``state`` (device int64[3]) holds the last refine index, the indicator value there (as
+  float64 bits: ``value``) and a running count of argmax calls whose winner was not finite
+  (``nonfinite``; argmax ranks NaN and +-inf first, so that is "some indicator entry was not
+  finite"), all written by dg_argmax_ex without a host sync."""
 
   def __init__(self, op):
     self.op = op
+    self.state = torch.zeros(3, dtype=torch.int64, device=op.device)
+    self.idx = self.state[0:1]
+    self.value = self.state[1:2].view(torch.float64)
+    self.nonfinite = self.state[2:3]
 
   def sum_rows(self, stacked):
     return sum_rows(stacked.contiguous(), stacked.shape[0])
 
   def argmax(self, x):
-    return self.op.argmax_async(x.contiguous(), use_abs=True)
+    return self.op.argmax_ex(x.contiguous(), self.idx, self.value, self.nonfinite, use_abs=True)
+
+
+def _exchange(coll, send, group, n_out=None):
+  """out = coll(out, send) over the process group.  RCCL ("nccl") moves device tensors over
+  xGMI directly; the gloo backend (several ranks on one GPU in tests) takes the exchange
+  through host copies, since gloo's all-to-all handles CPU tensors only."""
+  staged = send.is_cuda and dist.get_backend(group) == "gloo"
+  src = send.cpu() if staged else send
+  out = src.new_empty(src.numel() if n_out is None else n_out)
+  coll(out, src, group=group)
+  return out.to(send.device) if staged else out
 
 
 def gather_indicator(partial, n_total, reducer, group=None):
@@ -154,11 +183,9 @@ def gather_indicator(partial, n_total, reducer, group=None):
     chunk = -(-K // world)
     send = partial.new_zeros(world * chunk)
     send[:K] = partial.reshape(-1)
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)  # recv row r: rank r's slice
+    recv = _exchange(dist.all_to_all_single, send, group)  # recv row r: rank r's slice
     mine = reducer.sum_rows(recv.view(world, chunk))  # rank order
-    full = torch.empty_like(send)
-    dist.all_gather_into_tensor(full, mine.contiguous(), group=group)
+    full = _exchange(dist.all_gather_into_tensor, mine.contiguous(), group, world * chunk)
     total = full[:K]
   else:
     # one slice: its sum is itself
@@ -166,6 +193,18 @@ def gather_indicator(partial, n_total, reducer, group=None):
   # dividing by 1 is exact (bit-identical shortcut)
   mean = total / float(n_total) if n_total != 1 else total
   return mean, reducer.argmax(mean)
+
+
+_KEEP = {}
+
+
+def _keep_index(n_total, world, per, device):
+  """Rows of the padded all-gather that hold real ICs (cached per shape and device)."""
+  key = (n_total, world, per, str(device))
+  if key not in _KEEP:
+    keep = [r * per + i for r in range(world) for i in range(len(shard(n_total, r, world)))]
+    _KEEP[key] = torch.tensor(keep, device=device)
+  return _KEEP[key]
 
 
 def gather_per_ic(rows, n_total, group=None):
@@ -189,7 +228,8 @@ def gather_per_ic(rows, n_total, group=None):
   per = -(-n_total // world)
   send = rows.new_zeros(per, K)
   send[: rows.shape[0]] = rows
-  full = rows.new_empty(world * per, K)
-  dist.all_gather_into_tensor(full, send, group=group)
-  keep = [r * per + i for r in range(world) for i in range(len(shard(n_total, r, world)))]
-  return full[torch.tensor(keep, device=full.device)]
+  full = _exchange(dist.all_gather_into_tensor, send.reshape(-1), group,
+                   world * per * K).view(world * per, K)
+  if n_total % world == 0:  # no pad rows: the gathered block is the answer
+    return full
+  return full.index_select(0, _keep_index(n_total, world, per, full.device))

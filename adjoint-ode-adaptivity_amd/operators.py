@@ -214,16 +214,22 @@ class DGAdvection1D:
     _lib.check(rc, "dg_lserk4_fwd")
     return u
 
-  def adjoint(self, w, snapshots, t0, dt, nsteps, src_coef=0.0, eta=None):
+  def adjoint(self, w, snapshots, t0, dt, nsteps, src_coef=0.0, eta=None, eta_assign=False,
+              eta_abs=False):
     """Discrete adjoint sweep in place on w (terminal dJ/du^N in, dJ/du^0 out) and the
-    dual-weighted residual accumulated into eta (batch*K, caller-zeroed)."""
+    dual-weighted residual accumulated into eta (batch*K, caller-zeroed).
+
+    ``eta_assign``: eta is assigned instead of accumulated (no zero fill needed);
+    ``eta_abs``: eta ends as |eta| (Main_width_ref.py:139 ``jnp.abs(err)``).  Both are
+    folded into the sweep's first / last launch (dg_lserk4_adj_ex)."""
     eta_p = None if eta is None else self._field(eta, "eta", self.ktot)
-    rc = self._lib.dg_lserk4_adj(self._plan, self._field(w, "w"),
-                                 self._field(snapshots, "snapshots",
-                                             (nsteps + 1) * self.field_numel),
-                                 float(t0), float(dt), int(nsteps), float(src_coef), eta_p,
-                                 _stream(self.device))
-    _lib.check(rc, "dg_lserk4_adj")
+    flags = (_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) | (_lib.DG_ADJ_ETA_ABS if eta_abs else 0)
+    rc = self._lib.dg_lserk4_adj_ex(self._plan, self._field(w, "w"),
+                                    self._field(snapshots, "snapshots",
+                                                (nsteps + 1) * self.field_numel),
+                                    float(t0), float(dt), int(nsteps), float(src_coef), eta_p,
+                                    int(flags), _stream(self.device))
+    _lib.check(rc, "dg_lserk4_adj_ex")
     return w, eta
 
   def slope_limit(self, u, out=None, ids=None):
@@ -257,6 +263,23 @@ class DGAdvection1D:
   def argmax(self, x, use_abs=True):
     return int(self.argmax_async(x, use_abs).item())
 
+  def argmax_ex(self, x, idx, value=None, nonfinite=None, use_abs=True):
+    """argmax into ``idx`` (1-element CUDA int64) plus, on the device, the winning value into
+    ``value`` (1-element CUDA float64) and +1 into ``nonfinite`` (1-element CUDA int64) when
+    that value is not finite (dg_argmax_ex; no host sync)."""
+    n = x.numel()
+    if not x.is_cuda or x.dtype != torch.float64 or not x.is_contiguous():
+      raise TypeError("x must be a contiguous CUDA float64 tensor")
+    for t, name, dt_ in ((idx, "idx", torch.int64), (value, "value", torch.float64),
+                         (nonfinite, "nonfinite", torch.int64)):
+      if t is not None and (not t.is_cuda or t.dtype != dt_ or t.numel() < 1):
+        raise TypeError(f"{name} must be a CUDA {dt_} tensor")
+    ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rc = self._lib.dg_argmax_ex(self._plan, ctypes.c_void_p(x.data_ptr()), n, int(use_abs),
+                                ptr(idx), ptr(value), ptr(nonfinite), _stream(self.device))
+    _lib.check(rc, "dg_argmax_ex")
+    return idx
+
   def init_sine(self, amp, freq, phase, out=None):
     """u_b(x) = amp[b] sin(2 pi freq[b] x + phase[b]) on the device (ensemble ICs)."""
     out = self.new_field() if out is None else out
@@ -269,6 +292,21 @@ class DGAdvection1D:
                                 self._field(out, "u"), _stream(self.device))
     _lib.check(rc, "dg_init_sine")
     return out
+
+
+def stream_copy(src, dst):
+  """dst = src with the library's 16-byte-per-lane copy kernel (dg_stream_copy): the
+  achievable-HBM-bandwidth ceiling the bench reports."""
+  lib = _lib.load()
+  for t in (src, dst):
+    if not t.is_cuda or t.dtype != torch.float64 or not t.is_contiguous():
+      raise TypeError("stream_copy needs contiguous CUDA float64 tensors")
+  if src.numel() != dst.numel():
+    raise ValueError("src and dst differ in size")
+  rc = lib.dg_stream_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                          src.numel(), _stream(src.device))
+  _lib.check(rc, "dg_stream_copy")
+  return dst
 
 
 def sum_rows(x, rows, out=None):

@@ -1,9 +1,11 @@
 """Benchmark: DOF-updates/s of the 1D DG advection forward + adjoint sweep (BASELINE.json).
 
 One bench step = one forward sweep of --nsteps fused LSERK4 steps (snapshots stored),
-one adjoint sweep of --nsteps reverse steps accumulating the dual-weighted residual,
-the per-rank indicator reduction, the cross-rank rank-ordered sum (all-to-all + all-gather) + argmax
-(the refine decision), and the refine index copied to the host.
+one adjoint sweep of --nsteps reverse steps writing each trajectory's dual-weighted
+residual magnitude |eta| (DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS: no zero fill, no extra pass),
+the per-rank indicator reduction, the cross-rank rank-ordered sum (all-to-all + all-gather)
++ argmax (the refine decision, its value and a running non-finite count, all on the device),
+and the refine index + value copied to the host.
 
 Workload per rank = BASELINE config 2 (N=4, K=1,048,576, fp64, uniform mesh on [0,1],
 a = 2*pi, dt from One_code.mlx:111-112).  Rank 0 runs u0 = sin(2 pi x) (the golden IC);
@@ -11,13 +13,26 @@ rank j > 0 runs IC j of the synthetic ensemble.  N GPUs = an ensem
 trajectories, one per GPU (weak scaling; the only exchange is the indicator sum).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--nsteps S] [--no-cpu-baseline]
-  python bench.py --config 3     BASELINE config 3: Burgers-type flux + SlopeLimitN after
-                                 every stage, K = 4,194,304, one refine iteration per step
-                                 (fwd + adj + argmax + device split; replicas per GPU)
+  python bench.py --K 65536 --ics 1024   BASELINE config 4 (ensemble sharded over ranks,
+                                         strong scaling)
+  python bench.py --config 3             BASELINE config 3: Burgers-type flux + SlopeLimitN after
+                                         every stage, K = 4,194,304, one refine iteration per step
+                                         (fwd + adj + argmax + device split; replicas per GPU)
+  python bench.py --N n                  BASELINE config 5 (polynomial-order sweep)
+
+Multi-GPU: `--gpus N` without a launcher spawns N ranks itself (one process per GPU, before
+this process touches the GPU), each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1
+in its environment; under torch.distributed.run (WORLD_SIZE already set) it runs as that rank.
+
+Warm-up: at least --warmup steps, then more until the step time has converged (the GPU's
+clock ramps over the first ~30-60 ms of load, profiles/r02/ramp.json); the count is reported
+as `warmup_effective`.  The timed region is exactly --steps steps either way.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,17 +44,21 @@ if ROOT not in sys.path:
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec peak (AMD data sheet; not in the guide)
-PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
 
 
-def parse():
+def parse(argv=None):
   p = argparse.ArgumentParser()
   p.add_argument("--gpus", type=int, default=1)
   p.add_argument("--steps", type=int, default=None,
                  help="timed steps (default 100; config 3: 10 refine iterations)")
   p.add_argument("--warmup", type=int, default=None,
-                 help="untimed steps first (default 50, which also lets the GPU clocks settle; "
-                      "config 3: 8)")
+                 help="untimed steps first, at least (default 10; config 3: 4); more follow "
+                      "until the step time converges unless --no-converge")
+  p.add_argument("--no-converge", action="store_true",
+                 help="warm up exactly --warmup steps (no clock-ramp convergence)")
+  p.add_argument("--converge-min-ms", type=float, default=200.0,
+                 help="warm-up lasts at least this long (wall) before convergence is tested")
   p.add_argument("--N", type=int, default=4)
   p.add_argument("--config", type=int, default=2, choices=(2, 3),
                  help="2: linear advection (headline); 3: Burgers flux + limiter refine loop")
@@ -51,34 +70,87 @@ def parse():
   p.add_argument("--ics", type=int, default=0,
                  help="ensemble size over all ranks (config 4: --K 65536 --ics 1024); "
                       "default: one trajectory per rank (config 2 per GPU, weak scaling)")
+  p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                 help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo stages the "
+                      "exchange through host memory: for tests with several ranks on one GPU)")
   p.add_argument("--no-cpu-baseline", action="store_true")
   p.add_argument("--cpu-steps", type=int, default=12, help="time steps of the CPU sample")
   p.add_argument("--graph", action="store_true",
                  help="replay each sweep as a captured HIP graph (measured 1-3%% slower than "
                       "eager launches on this path, profiles/r01/bench_eager_vs_graph.txt)")
-  a = p.parse_args()
+  a = p.parse_args(argv)
   # Config 3 refines one element per step, so its step count is bounded by how often the
   # loop can split the same region before the element width reaches fp64 resolution.
   if a.steps is None:
     a.steps = 10 if a.config == 3 else 100
   if a.warmup is None:
-    a.warmup = 8 if a.config == 3 else 50
+    a.warmup = 4 if a.config == 3 else 10
   return a
 
 
+# ---------------------------------------------------------------------------
+# Multi-rank launch: one process per GPU (the reference's own multi-GPU pattern is one
+# process per GPU from its launcher, python/Submit_schedule_frontera/
+# Generating_argurment_files.py:23-36).  Nothing here touches the GPU.
+# ---------------------------------------------------------------------------
+def free_port():
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    return s.getsockname()[1]
+
+
+def spawn_ranks(nprocs, argv, script=None, env_extra=None, poll_s=0.2):
+  """Run `script argv` as ranks 0..nprocs-1 (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set),
+  rank 0's stdout passed through, the others' discarded (they print nothing), everyone's
+  stderr passed through.  If a rank fails, the others are terminated (by handle).  Returns
+  the first non-zero exit code, else 0."""
+  script = script or os.path.abspath(__file__)
+  port = free_port()
+  procs = []
+  for r in range(nprocs):
+    env = dict(os.environ)
+    env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nprocs),
+                "LOCAL_WORLD_SIZE": str(nprocs), "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.update(env_extra or {})
+    out = None if r == 0 else subprocess.DEVNULL
+    procs.append(subprocess.Popen([sys.executable, script, *argv], env=env, stdout=out))
+  rc = 0
+  live = list(procs)
+  while live:
+    for p in list(live):
+      code = p.poll()
+      if code is None:
+        continue
+      live.remove(p)
+      if code != 0 and rc == 0:
+        rc = code
+        for q in live:
+          q.terminate()
+    time.sleep(poll_s)
+  for p in procs:
+    p.wait()
+  return rc
+
+
 def stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
-  """Achievable HBM bandwidth on this box: a device-to-device copy of
-  `nbytes` (read + write counted), median over `reps`, timed with HIP events."""
+  """Achievable HBM bandwidth on this box: the library's 16-byte-per-lane copy
+  kernel (dg_stream_copy) over `nbytes` (read + write counted), median over `reps`, timed
+  with HIP events on the stream it runs on."""
+  import importlib
+
   import torch
+  ops = importlib.import_module("adjoint-ode-adaptivity_amd.operators")
   src = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).fill_(1.0)
   dst = torch.empty_like(src)
   st = torch.cuda.current_stream(dev)
-  dst.copy_(src)
+  for _ in range(3):
+    ops.stream_copy(src, dst)
   ts = []
   for _ in range(reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    dst.copy_(src)
+    ops.stream_copy(src, dst)
     e1.record(st)
     e1.synchronize()
     ts.append(e0.elapsed_time(e1) * 1e-3)
@@ -136,24 +208,123 @@ def cpu_baseline_config3(N, K, nsteps):
                     f"stands for both directions"}
 
 
+def warm_up(step, args, stream, max_steps, block=10):
+  """--warmup steps, then blocks of `block` steps until (a) --converge-min-ms of wall time
+  has passed and (b) the last block's device time is within 1 % of the previous block's and
+  of the fastest block so far -- the GPU's clock ramps over the first tens of ms of load
+  (profiles/r02/ramp.json) -- or `max_steps` is reached.  Returns (steps run, wall ms,
+  last block ms per step)."""
+  import torch
+  t0 = time.perf_counter()
+  n = 0
+  for _ in range(args.warmup):
+    step()
+    n += 1
+  if args.no_converge:
+    torch.cuda.synchronize()
+    return n, (time.perf_counter() - t0) * 1e3, None
+  best = prev = None
+  last = None
+  while n + block <= max_steps:
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(block):
+      step()
+    e1.record(stream)
+    e1.synchronize()
+    n += block
+    last = e0.elapsed_time(e1) / block
+    waited = (time.perf_counter() - t0) * 1e3 >= args.converge_min_ms
+    if (waited and prev is not None and abs(last - prev) <= 0.01 * prev
+        and last <= 1.01 * best):
+      break
+    best = last if best is None else min(best, last)
+    prev = last
+  return n, (time.perf_counter() - t0) * 1e3, last
+
+
+def stats(xs):
+  xs = np.asarray(xs, dtype=float)
+  return {"first": float(xs[0]), "median": float(np.median(xs)), "last": float(xs[-1]),
+          "min": float(xs.min()), "max": float(xs.max())}
+
+
+def init_dist(args):
+  import torch
+  import torch.distributed as dist
+  world = int(os.environ.get("WORLD_SIZE", "1"))
+  rank = int(os.environ.get("RANK", "0"))
+  local = int(os.environ.get("LOCAL_RANK", "0"))
+  ndev = torch.cuda.device_count()
+  if ndev < 1:
+    raise RuntimeError("bench.py needs a ROCm GPU")
+  torch.cuda.set_device(local % ndev)
+  dev = torch.device("cuda", local % ndev)
+  if world > 1:
+    if args.backend == "nccl":
+      dist.init_process_group("nccl", device_id=dev)
+    else:
+      dist.init_process_group("gloo")
+  return world, rank, dev
+
+
+def ranks_agree(value, world, dev, backend):
+  """All ranks' values (ints), gathered to every rank."""
+  if world == 1:
+    return [int(value)]
+  import torch
+  import torch.distributed as dist
+  d = dev if backend == "nccl" else torch.device("cpu")
+  mine = torch.tensor([int(value)], dtype=torch.int64, device=d)
+  allv = torch.empty(world, dtype=torch.int64, device=d)
+  dist.all_gather_into_tensor(allv, mine)
+  return [int(v) for v in allv.cpu()]
+
+
+def max_over_ranks(x, world, dev, backend):
+  if world == 1:
+    return float(x)
+  import torch
+  import torch.distributed as dist
+  d = dev if backend == "nccl" else torch.device("cpu")
+  t = torch.tensor([float(x)], dtype=torch.float64, device=d)
+  dist.all_reduce(t, op=dist.ReduceOp.MAX)
+  return float(t.item())
+
+
+def sum_over_ranks(x, world, dev, backend):
+  if world == 1:
+    return float(x)
+  import torch
+  import torch.distributed as dist
+  d = dev if backend == "nccl" else torch.device("cpu")
+  t = torch.tensor([float(x)], dtype=torch.float64, device=d)
+  dist.all_reduce(t)
+  return float(t.item())
+
+
+def barrier(world):
+  if world > 1:
+    import torch.distributed as dist
+    dist.barrier()
+
+
 def main_config3(args, world, rank, dev):
   """Config 3: one refine iteration per bench step on a trajectory of K elements (each
   rank an independent replica; no data-path collective)."""
   import importlib
 
   import torch
-  import torch.distributed as dist
   pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
   N, K, nsteps = args.N, args.K or (1 << 22), args.nsteps
+  max_warm = args.warmup + 60
   mesh = pkg.BaseGalerkin1D(n=N, k=K, domain=[0.0, 1.0])
-  run = pkg.adaptive.AdaptiveSweep(mesh, nsteps, args.warmup + args.steps + 1,
+  run = pkg.adaptive.AdaptiveSweep(mesh, nsteps, max_warm + args.steps + 1,
                                    flux="burgers", limiter=True)
   stream = torch.cuda.current_stream(dev)
-  for _ in range(args.warmup):
-    run.iterate()
+  warm, warm_ms, _ = warm_up(lambda: run.iterate(), args, stream, max_warm, block=4)
   torch.cuda.synchronize()
-  if world > 1:
-    dist.barrier()
+  barrier(world)
   torch.cuda.synchronize()
   evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
   total = 0
@@ -170,22 +341,18 @@ def main_config3(args, world, rank, dev):
     total += run.refine()
     ref_idx = run.sync()
   torch.cuda.synchronize()
-  if world > 1:
-    dist.barrier()
+  barrier(world)
   torch.cuda.synchronize()
-  elapsed = time.perf_counter() - t0
-  if world > 1:
-    t = torch.tensor([elapsed, float(total)], dtype=torch.float64, device=dev)
-    dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
-    dist.all_reduce(t[1:2])
-    elapsed, total = float(t[0].item()), float(t[1].item())
+  elapsed = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
+  total = sum_over_ranks(total, world, dev, args.backend)
   Np = N + 1
-  k_mid = K + args.warmup + args.steps // 2
+  k_mid = K + warm + args.steps // 2
   # forward steps per launch with snapshots (dg_burgers.hip chunk_nl): 2 only when tuned to 2
   ms = 2 if run.op.steps_per_launch == 2 else 1
   fwd_launches = (nsteps + ms - 1) // ms
-  fwd_us = float(np.mean([e[0].elapsed_time(e[1]) for e in evs])) * 1e3 / fwd_launches
-  adj_us = float(np.mean([e[2].elapsed_time(e[3]) for e in evs])) * 1e3 / nsteps
+  fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / fwd_launches for e in evs]
+  adj_us = [e[2].elapsed_time(e[3]) * 1e3 / nsteps for e in evs]
+  fwd_m, adj_m = float(np.mean(fwd_us)), float(np.mean(adj_us))
   # Algorithmic bytes per launch: forward reads u^n once and writes ms snapshots; the
   # adjoint (one step per launch) reads w^{n+1} and u^n, writes w^n, updates eta.
   fwd_bytes = (8.0 + 8.0 * ms) * Np * k_mid
@@ -197,6 +364,8 @@ def main_config3(args, world, rank, dev):
       "n_gpus": world,
       "steps": args.steps,
       "warmup": args.warmup,
+      "warmup_effective": warm,
+      "warmup_ms": warm_ms,
       "ms_per_step": elapsed / args.steps * 1e3,
       "higher_is_better": True,
       "scaling": "weak",
@@ -207,18 +376,21 @@ def main_config3(args, world, rank, dev):
                               f"stage, N={N}, K={K}+refinements, {nsteps}+{nsteps} steps/sweep "
                               f"+ DWR indicator + argmax + device element split per step"),
                  "N": N, "K": K, "nsteps_per_sweep": nsteps, "parallelism": f"replicas{world}"},
-      "roofline": {"bound": "hbm", "achieved": adj_bytes / (adj_us * 1e-6) / 1e9,
+      "roofline": {"bound": "hbm", "achieved": adj_bytes / (adj_m * 1e-6) / 1e9,
                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": adj_bytes / (adj_us * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                   "frac": adj_bytes / (adj_m * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                    "kernel": f"k_adj_nl<{Np},burgers,limiter,nonuniform> (1 reverse step + "
                              f"stage recompute + DWR per launch)",
-                   "launch_us": adj_us, "algorithmic_bytes": adj_bytes},
-      "roofline_fwd": {"bound": "hbm", "achieved": fwd_bytes / (fwd_us * 1e-6) / 1e9,
+                   "launch_us": adj_m, "launch_us_stats": stats(adj_us),
+                   "algorithmic_bytes": adj_bytes},
+      "roofline_fwd": {"bound": "hbm", "achieved": fwd_bytes / (fwd_m * 1e-6) / 1e9,
                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": fwd_bytes / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                       "frac": fwd_bytes / (fwd_m * 1e-6) / 1e9 / HBM_PEAK_GBS,
                        "kernel": f"k_step_nl<{Np},burgers,limiter,nonuniform,{ms}>",
-                       "launch_us": fwd_us, "algorithmic_bytes": fwd_bytes},
+                       "launch_us": fwd_m, "launch_us_stats": stats(fwd_us),
+                       "algorithmic_bytes": fwd_bytes},
       "refine_index": ref_idx,
+      "refine_index_ranks": ranks_agree(ref_idx, world, dev, args.backend),
       "K_final": run.K,
   }
   if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -226,25 +398,36 @@ def main_config3(args, world, rank, dev):
   if rank == 0:
     print(json.dumps(out), flush=True)
   if world > 1:
+    import torch.distributed as dist
     dist.destroy_process_group()
 
 
-def main():
-  args = parse()
+def launches_per_sweep(nsteps, ms):
+  """The library's greedy chunking of a sweep into launches of <= ms steps."""
+  launches, left = 0, nsteps
+  while left > 0:
+    m = ms
+    while m > left:
+      m //= 2
+    left -= m
+    launches += 1
+  return launches
+
+
+def main(argv=None):
+  args = parse(argv)
+  if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    # Self-launch: one rank per GPU, started before this process touches the GPU.
+    sys.exit(spawn_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv)))
   import torch
-  import torch.distributed as dist
 
   import importlib
   pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
   ens = pkg.ensemble
 
-  world = int(os.environ.get("WORLD_SIZE", "1"))
-  rank = int(os.environ.get("RANK", "0"))
-  local = int(os.environ.get("LOCAL_RANK", "0"))
-  torch.cuda.set_device(local)
-  if world > 1:
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-  dev = torch.device("cuda", local)
+  world, rank, dev = init_dist(args)
+  if args.gpus > 1 and world != args.gpus:
+    raise RuntimeError(f"--gpus {args.gpus} but WORLD_SIZE = {world}")
   if args.config == 3:
     return main_config3(args, world, rank, dev)
 
@@ -261,12 +444,11 @@ def main():
               else ens.ic_params([rank]))
     n_total = world
   sweep = ens.EnsembleSweep(mesh, ics, nsteps, dt, params=params)
-  reducer = ens.DeviceReducer(sweep.op)
+  reducer = ens.DeviceReducer(sweep.op)  # argmax + value + non-finite count on the device
   if args.graph:
     sweep.capture()  # each sweep becomes one HIP graph launch
   stream = torch.cuda.current_stream(dev)
-  idx_host = torch.zeros(1, dtype=torch.int64).pin_memory()
-  val_host = torch.zeros(1, dtype=torch.float64).pin_memory()
+  res_host = torch.zeros(2, dtype=torch.int64).pin_memory()  # refine index, value bits
 
   def one_step(ev=None):
     if ev:
@@ -274,66 +456,52 @@ def main():
     sweep.forward_graph() if args.graph else sweep.forward()
     if ev:
       ev[1].record(stream)
-    if args.graph:
-      if ev:
-        ev[2].record(stream)
-      sweep.adjoint_graph()
-    else:  # eta's zero fill stays outside the adjoint kernels' bracket
-      sweep.eta.zero_()
-      if ev:
-        ev[2].record(stream)
-      sweep.run_adjoint()
+    sweep.adjoint_graph() if args.graph else sweep.run_adjoint()
     if ev:
-      ev[3].record(stream)
+      ev[2].record(stream)
     partial = sweep.reduce()
-    mean, idx = ens.gather_indicator(partial, n_total, reducer)
+    ens.gather_indicator(partial, n_total, reducer)
     if args.gather_ics:
       ens.gather_per_ic(sweep.per_ic(), n_total)
-    # The refine index goes to the host (the mesh split's input) without stalling the
-    # stream: an async copy into pinned memory, read once the timed region has synced.
-    # The indicator there is finite iff it is finite everywhere (argmax ranks NaN first).
-    idx_host.copy_(idx, non_blocking=True)
-    val_host.copy_(mean.index_select(0, idx), non_blocking=True)
+    # The refine index (the mesh split's input) and the indicator there go to the host in
+    # one async copy into pinned memory, read after the timed region has synced.
+    res_host.copy_(reducer.state[0:2], non_blocking=True)
 
-  for _ in range(args.warmup):
-    one_step()
+  warm, warm_ms, warm_last = warm_up(one_step, args, stream, max_steps=args.warmup + 600)
   torch.cuda.synchronize()
-  if world > 1:
-    dist.barrier()
+  reducer.nonfinite.zero_()  # count non-finite indicators over the timed steps only
+  barrier(world)
   torch.cuda.synchronize()
 
-  evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+  evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+  ev_end = torch.cuda.Event(enable_timing=True)
   t0 = time.perf_counter()
   for s in range(args.steps):
     one_step(evs[s])
+  ev_end.record(stream)
   host_issue = time.perf_counter() - t0  # host time to enqueue the steps (launch-bound check)
   torch.cuda.synchronize()
-  ref_idx = int(idx_host.item())
-  pkg.adaptive.check_indicator(float(val_host.item()), ref_idx)
-  if world > 1:
-    dist.barrier()
+  barrier(world)
   torch.cuda.synchronize()
   elapsed = time.perf_counter() - t0
-  if world > 1:
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+  elapsed = max_over_ranks(elapsed, world, dev, args.backend)
 
-  fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-  adj_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+  ref_idx = int(res_host[0])
+  ref_val = float(res_host[1:2].view(torch.float64)[0])
+  nonfinite = int(reducer.nonfinite.item())
+  if nonfinite:
+    pkg.adaptive.check_indicator(float("nan"), ref_idx)  # raises FloatingPointError
+  pkg.adaptive.check_indicator(ref_val, ref_idx)
+
   Np, ktot = N + 1, K * sweep.batch
   ms = sweep.op.steps_per_launch
-  launches = 0
-  left = nsteps
-  while left > 0:  # the library's greedy chunking of a sweep into launches
-    m = ms
-    while m > left:
-      m //= 2
-    left -= m
-    launches += 1
-  fwd_launch_us = fwd_ms * 1e3 / launches
-  adj_launch_us = adj_ms * 1e3 / launches
-  # Algorithmic bytes per launch of `ms` fused steps (DESIGN.md §Roofline):
+  launches = launches_per_sweep(nsteps, ms)
+  fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / launches for e in evs]
+  adj_us = [e[1].elapsed_time(e[2]) * 1e3 / launches for e in evs]
+  step_ms = [evs[i][0].elapsed_time(evs[i + 1][0] if i + 1 < len(evs) else ev_end)
+             for i in range(len(evs))]
+  fwd_launch_us, adj_launch_us = float(np.mean(fwd_us)), float(np.mean(adj_us))
+  # Algorithmic bytes per launch of `ms` fused steps (DESIGN.md §5):
   #   forward: read u^n once, write the ms snapshots u^{n+1..n+ms}:  (8 + 8 ms) B per DOF
   #   adjoint: read w^{n+ms}, read the ms snapshots, write w^n: (16 + 8 ms) B per DOF,
   #            plus the indicator read-modify-write, 16 B per element.
@@ -341,24 +509,19 @@ def main():
   adj_bytes = (16.0 + 8.0 * ms) * Np * ktot + 16.0 * ktot
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
-  traffic = None
-  traffic_src = None
+  traffic = traffic_src = None
   if os.path.exists(PROFILE_TRAFFIC):
     try:
       with open(PROFILE_TRAFFIC) as f:
         tr = json.load(f)
-      if tr.get("N") == N and tr.get("K") == K and tr.get("steps_per_launch") == ms:
+      if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
+          and tr.get("steps_per_launch") == ms):
         traffic = tr.get("adj_bytes_per_launch")
         traffic_src = tr.get("source")
     except (OSError, ValueError):
       pass
 
-  if world > 1:
-    d = torch.tensor([float(sweep.dof_updates)], dtype=torch.float64, device=dev)
-    dist.all_reduce(d)
-    total_dofs = float(d.item()) * args.steps
-  else:
-    total_dofs = sweep.dof_updates * args.steps
+  total_dofs = sum_over_ranks(sweep.dof_updates, world, dev, args.backend) * args.steps
   value = total_dofs / elapsed
   # The single-step algorithm moves 16 B (fwd) + 24 B + 16/Np B (adj) per pair of
   # DOF-updates, so its HBM roofline is 8 TB/s / that per-update average.
@@ -367,6 +530,9 @@ def main():
   # SURVEY §8d's algorithmic flop count, 5 (2 Np + 11) per DOF-update (both directions).
   flop_per_update = 5.0 * (2 * Np + 11)
   copy_gbs = stream_copy_gbs(dev) if rank == 0 else None
+  import torch.distributed as dist
+  dist_world = dist.get_world_size() if dist.is_initialized() else 1
+  idx_ranks = ranks_agree(ref_idx, world, dev, args.backend)
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
       "value": value,
@@ -374,6 +540,9 @@ def main():
       "n_gpus": world,
       "steps": args.steps,
       "warmup": args.warmup,
+      "warmup_effective": warm,
+      "warmup_ms": warm_ms,
+      "warmup_last_step_ms": warm_last,
       "ms_per_step": elapsed / args.steps * 1e3,
       "higher_is_better": True,
       "scaling": "strong" if args.ics > 0 else "weak",
@@ -389,12 +558,14 @@ def main():
       "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
                    "kernel": f"k_adj<{Np},5,uniform,{sweep.op.tile_width},{ms}> ({ms} reverse steps + DWR per launch)",
-                   "launch_us": adj_launch_us, "algorithmic_bytes": adj_bytes,
-                   "traffic_source": traffic_src},
+                   "launch_us": adj_launch_us, "launch_us_stats": stats(adj_us),
+                   "algorithmic_bytes": adj_bytes, "traffic_source": traffic_src},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_gbs / HBM_PEAK_GBS,
                        "kernel": f"k_step<{Np},5,uniform,{sweep.op.tile_width},{ms}> ({ms} steps per launch)",
-                       "launch_us": fwd_launch_us, "algorithmic_bytes": fwd_bytes},
+                       "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
+                       "algorithmic_bytes": fwd_bytes},
+      "step_ms_stats": stats(step_ms),
       "single_step_roofline": {"value": single_step_roofline, "unit": "DOF-updates/s",
                                "bytes_per_update": single_step_bytes,
                                "frac": value / single_step_roofline},
@@ -403,18 +574,28 @@ def main():
                 "peak_fp64_vector_tflops_per_gpu": FP64_PEAK_TFLOPS,
                 "frac": value * flop_per_update / 1e12 / (FP64_PEAK_TFLOPS * world)},
       "stream_copy": {"achievable_GBs": copy_gbs, "unit": "GB/s",
-                      "what": "1 GiB device-to-device copy, read + write, rank 0",
-                      "adj_frac_of_achievable": adj_gbs / copy_gbs if copy_gbs else None},
+                      "what": "dg_stream_copy (16 B per lane, 4 in flight) of 1 GiB, read + "
+                              "write, rank 0",
+                      "adj_frac_of_achievable": adj_gbs / copy_gbs if copy_gbs else None,
+                      "fwd_frac_of_achievable": fwd_gbs / copy_gbs if copy_gbs else None},
       "steps_per_launch": ms,
       "refine_index": ref_idx,
+      "refine_value": ref_val,
+      "refine_index_ranks": idx_ranks,
+      "nonfinite_indicator_steps": nonfinite,
+      "collective_backend": args.backend if world > 1 else None,
+      "rccl_world_size": dist_world,
       "host_issue_ms_per_step": host_issue / args.steps * 1e3,
   }
+  if len(set(idx_ranks)) != 1:
+    raise RuntimeError(f"refine index differs across ranks: {idx_ranks}")
   if rank == 0 and world == 1 and args.ics == 0 and not args.no_cpu_baseline:
     out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_steps)
     out["cpu_baseline_8t"] = cpu_baseline(N, K, args.cpu_steps, threads=8)
   if rank == 0:
     print(json.dumps(out), flush=True)
   if world > 1:
+    import torch.distributed as dist
     dist.destroy_process_group()
 
 

@@ -157,6 +157,16 @@ int dg_lserk4_fwd(dg_plan* plan, double* u, double t0, double dt, int nsteps,
 int dg_lserk4_adj(dg_plan* plan, double* w, const double* snapshots, double t0, double dt,
                   int nsteps, double src_coef, double* eta, void* stream);
 
+/* dg_lserk4_adj with indicator write flags (bit-identical results; fewer passes over eta):
+ *   DG_ADJ_ETA_ASSIGN  the sweep's first launch assigns eta instead of adding to it, so the
+ *                      caller need not zero it (nsteps = 0: eta is zeroed)
+ *   DG_ADJ_ETA_ABS     the sweep's last launch stores |eta|: the per-trajectory magnitude the
+ *                      reference's errorIndicator returns (python/Main_width_ref.py:139,
+ *                      `return jnp.abs(err)`) before its mean over ICs (:479) */
+enum { DG_ADJ_ETA_ASSIGN = 1, DG_ADJ_ETA_ABS = 2 };
+int dg_lserk4_adj_ex(dg_plan* plan, double* w, const double* snapshots, double t0, double dt,
+                     int nsteps, double src_coef, double* eta, int flags, void* stream);
+
 /* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */
 int dg_slope_limit_n(dg_plan* plan, const double* u, double* ulim, int32_t* ids_mask,
@@ -171,6 +181,19 @@ int dg_slope_limit_1(dg_plan* plan, const double* u, double* ulim, void* stream)
  * idx is a device int64.  n <= batch*K of the plan (scratch is sized by it). */
 int dg_argmax(dg_plan* plan, const double* x, int64_t n, int use_abs, int64_t* idx,
               void* stream);
+
+/* dg_argmax plus the winning value and a non-finite count, all on the device (no host sync):
+ * value (nullable device double) = x[idx] (|x[idx]| when use_abs); nonfinite_count (nullable
+ * device int64) is incremented when that value is NaN or +-inf.  Under use_abs the winner is
+ * non-finite exactly when some |x| is (NaN ranks first, +inf above every finite value), so a
+ * count accumulated over many calls says whether any of them saw a non-finite indicator.
+ * (Failure-detection role of the reference's "did not converge" messages, dg_march.m:71-73.) */
+int dg_argmax_ex(dg_plan* plan, const double* x, int64_t n, int use_abs, int64_t* idx,
+                 double* value, int64_t* nonfinite_count, void* stream);
+
+/* dst[0:n] = src[0:n] with 16-byte device loads and stores (both 16-byte aligned): the
+ * achievable-HBM-bandwidth ceiling of SURVEY 8(d) ("measured with a stream-copy kernel"). */
+int dg_stream_copy(const double* src, double* dst, int64_t n, void* stream);
 
 /* out[k] = sum_{r=0}^{rows-1} x[r*n + k], summed in ascending r (bit-reproducible).
  * Ensemble reduction of per-IC indicators (python/Main_width_ref.py:479 mean-over-ICs role). */

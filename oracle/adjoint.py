@@ -145,6 +145,14 @@ def sum_rows(x):
   return acc
 
 
+def ensemble_indicator(rows):
+  """The ensemble refine indicator: the mean over ICs of each IC's |eta| (the reference's
+  errorIndicator returns jnp.abs(err) per IC, python/Main_width_ref.py:139; the mean over
+  ICs is :479, the refine index its argmax + 1, :491), summed in IC order."""
+  rows = np.asarray(rows)
+  return sum_rows(np.abs(rows)) / float(rows.shape[0])
+
+
 def argmax(x, use_abs=False):
   """numpy.argmax semantics (first index on ties, NaN is maximal) — dg_argmax."""
   x = np.asarray(x)

@@ -39,6 +39,7 @@ def main():
   p.add_argument("--N", type=int, default=4)
   p.add_argument("--K", type=int, default=1 << 20)
   p.add_argument("--steps-per-launch", type=int, default=4)
+  p.add_argument("--batch", type=int, default=1)
   a = p.parse_args()
   out = collections.OrderedDict()
   for r in csv.DictReader(open(a.stats)):
@@ -62,7 +63,8 @@ def main():
       return None
     adj = [k for k in out if k.startswith("k_adj")]
     fwd = [k for k in out if k.startswith("k_step")]
-    tr = {"N": a.N, "K": a.K, "steps_per_launch": a.steps_per_launch, "source": a.out,
+    tr = {"N": a.N, "K": a.K, "batch": a.batch, "steps_per_launch": a.steps_per_launch,
+          "source": a.out,
           "adj_kernel": adj[0] if adj else None,
           "adj_bytes_per_launch": hbm(adj[0]) if adj else None,
           "fwd_kernel": fwd[0] if fwd else None,

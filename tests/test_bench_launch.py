@@ -1,0 +1,70 @@
+"""bench.py's self-launch (`--gpus N` without torch.distributed.run): N ranks, one process
+each, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1 in their environment, rank 0's one
+JSON line passed through, a failing rank ending the job with its exit code.  CPU only: the
+ranks here run a gloo stand-in for the bench body (the GPU body is covered by
+tests/test_gpu_bench.py); bench's own argument parsing and the spawn are the product code."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+CHILD = r'''
+import json, os, sys
+import torch, torch.distributed as dist
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+assert os.environ["MASTER_ADDR"] == "127.0.0.1"
+assert int(os.environ["LOCAL_RANK"]) == rank
+dist.init_process_group("gloo")
+mine = torch.tensor([100 + 7 * (rank % 1)], dtype=torch.int64)  # same "refine index" on all
+allv = torch.empty(world, dtype=torch.int64)
+dist.all_gather_into_tensor(allv, mine)
+fail_rank = int(sys.argv[1]) if len(sys.argv) > 1 else -1
+if rank == fail_rank:
+    sys.exit(3)
+if rank == 0:
+    print(json.dumps({"n_gpus": dist.get_world_size(), "refine_index_ranks": allv.tolist()}))
+dist.destroy_process_group()
+'''
+
+
+def _bench():
+  sys.path.insert(0, ROOT)
+  import importlib
+  return importlib.import_module("bench")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_spawn_ranks_one_json_line(tmp_path, world):
+  child = tmp_path / "child.py"
+  child.write_text(CHILD)
+  code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+          f"sys.exit(bench.spawn_ranks({world}, [], script={str(child)!r}))")
+  r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+  assert r.returncode == 0, r.stderr
+  # (gloo itself prints "[Gloo] Rank 0 is connected ..." lines; RCCL prints none)
+  lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+  assert len(lines) == 1
+  out = json.loads(lines[0])
+  assert out["n_gpus"] == world
+  assert len(set(out["refine_index_ranks"])) == 1 and len(out["refine_index_ranks"]) == world
+
+
+def test_spawn_ranks_propagates_a_failure(tmp_path):
+  child = tmp_path / "child.py"
+  child.write_text(CHILD)
+  code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+          f"sys.exit(bench.spawn_ranks(2, ['1'], script={str(child)!r}))")
+  r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+  assert r.returncode == 3
+
+
+def test_bench_arguments():
+  b = _bench()
+  a = b.parse(["--gpus", "8", "--steps", "20", "--warmup", "5"])
+  assert (a.gpus, a.steps, a.warmup, a.config, a.backend) == (8, 20, 5, 2, "nccl")
+  assert b.parse(["--config", "3"]).steps == 10
+  assert b.launches_per_sweep(20, 4) == 5 and b.launches_per_sweep(7, 4) == 3

@@ -33,9 +33,10 @@ def _free_port():
 
 
 def _partials(world, K=1001, n_ics=12):
-  """Per-IC indicator rows (deterministic), summed per rank in fixed order."""
+  """Per-IC indicator magnitudes (deterministic signed rows, then |.| per IC as the
+  adjoint's DG_ADJ_ETA_ABS stores them), summed per rank in fixed order."""
   rng = np.random.default_rng(0)
-  rows = rng.standard_normal((n_ics, K)) * 10.0 ** rng.integers(-6, 3, (n_ics, K))
+  rows = np.abs(rng.standard_normal((n_ics, K)) * 10.0 ** rng.integers(-6, 3, (n_ics, K)))
   import importlib
   import sys
   sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -69,6 +70,8 @@ def test_gather_indicator_rank_order_and_identical_on_all_ranks(world):
   _, parts = _partials(world)
   from oracle import adjoint as oadj
   expect = oadj.sum_rows(np.stack(parts)) / 12.0
+  rows, _ = _partials(1)
+  np.testing.assert_allclose(expect, oadj.ensemble_indicator(rows), rtol=1e-13)
   for r in range(world):
     mean, idx = out[r]
     np.testing.assert_array_equal(mean, expect)  # bit-identical on every rank
@@ -112,3 +115,38 @@ def test_gather_per_ic_rows_in_ic_order_on_every_rank(world, n_ics):
   rows, _ = _partials(world, n_ics=n_ics)
   for r in range(world):
     np.testing.assert_array_equal(out[r], rows)
+
+
+def _worker_signs(rank, world, port, out):
+  os.environ["MASTER_ADDR"] = "127.0.0.1"
+  os.environ["MASTER_PORT"] = str(port)
+  dist.init_process_group("gloo", rank=rank, world_size=world)
+  try:
+    import importlib
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    ens = importlib.import_module("adjoint-ode-adaptivity_amd.ensemble")
+    signed = _opposite_sign_rows()
+    mine = np.abs(signed[list(ens.shard(2, rank, world))])  # |eta_ic| per IC (ETA_ABS)
+    mean, idx = ens.gather_indicator(torch.from_numpy(mine.sum(axis=0)), 2, OracleReducer())
+    out[rank] = int(idx[0])
+  finally:
+    dist.destroy_process_group()
+
+
+def _opposite_sign_rows():
+  """Two ICs whose signed indicators cancel at element 0: the signed mean would refine
+  element 2, the reference's mean of magnitudes (Main_width_ref.py:139,479) element 0."""
+  return np.array([[5.0, 0.5, 1.0, 0.1],
+                   [-5.0, 0.5, 1.0, 0.1]])
+
+
+def test_opposite_signed_ics_do_not_cancel():
+  signed = _opposite_sign_rows()
+  from oracle import adjoint as oadj
+  assert int(np.argmax(np.abs(signed.mean(axis=0)))) == 2  # what a signed sum would pick
+  assert oadj.argmax(oadj.ensemble_indicator(signed), use_abs=True) == 0
+  mgr = mp.Manager()
+  out = mgr.dict()
+  mp.spawn(_worker_signs, args=(2, _free_port(), out), nprocs=2, join=True)
+  assert out[0] == out[1] == 0

@@ -1,0 +1,128 @@
+"""Round-2 ABI additions, through ctypes on the GPU: the adjoint's indicator write flags
+(dg_lserk4_adj_ex), the ensemble's per-IC magnitudes, dg_argmax_ex's device-side value and
+non-finite count, and the dg_stream_copy bandwidth kernel.
+
+Bars: the flags change no arithmetic, so flagged and unflagged sweeps agree bit for bit
+(|x| of the same bits); argmax indices exact; the copy exact.
+"""
+import numpy as np
+import pytest
+
+from oracle import adjoint as oadj
+from oracle import advec as oadv
+from oracle import setup1d
+
+pytestmark = pytest.mark.gpu
+
+
+def host(t):
+  return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("physics", ["linear", "burgers_limited"])
+def test_adjoint_eta_flags_are_bit_identical(pkg, gpu, physics):
+  import torch
+  N, K, nsteps = 4, 333, 7
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  kw = {} if physics == "linear" else dict(flux="burgers", limiter=True)
+  op = pkg.operators.DGAdvection1D(mesh, **kw)
+  dt = mesh.cfl_dt() * (1.0 if physics == "linear" else 0.5)
+  snaps = op.new_field(nsteps + 1)
+  op.init_sine([0.9], [2.0], [0.3], out=snaps[0])
+  op.forward(snaps[0], 0.0, dt, nsteps, snaps)
+  g = snaps[nsteps].clone()
+  w0, eta0 = g.clone(), torch.zeros(K, dtype=torch.float64, device=gpu)
+  op.adjoint(w0, snaps, 0.0, dt, nsteps, src_coef=0.3, eta=eta0)
+  w1 = g.clone()
+  eta1 = torch.full((K,), float("nan"), dtype=torch.float64, device=gpu)  # assign overwrites
+  op.adjoint(w1, snaps, 0.0, dt, nsteps, src_coef=0.3, eta=eta1, eta_assign=True, eta_abs=True)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(host(w1), host(w0))
+  np.testing.assert_array_equal(host(eta1), np.abs(host(eta0)))
+  assert (host(eta0) < 0).any() and (host(eta0) > 0).any()  # both signs occur
+
+
+def test_eta_assign_with_zero_steps_zeroes(pkg, gpu):
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=3, k=64)
+  op = pkg.operators.DGAdvection1D(mesh)
+  snaps = op.new_field(1)
+  op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
+  eta = torch.full((64,), 7.0, dtype=torch.float64, device=gpu)
+  op.adjoint(snaps[0].clone(), snaps, 0.0, 1e-3, 0, eta=eta, eta_assign=True)
+  torch.cuda.synchronize()
+  assert not host(eta).any()
+
+
+def test_ensemble_rows_are_per_ic_magnitudes(pkg, gpu):
+  """EnsembleSweep rows = |signed eta| of each IC run alone (Main_width_ref.py:139), their
+  rank partial = the IC-order sum of the magnitudes, and the refine index = argmax of the
+  oracle's ensemble_indicator of the signed rows."""
+  import torch
+  K, ics, nsteps = 256, [1, 2, 5, 6], 8
+  mesh = pkg.BaseGalerkin1D(n=4, k=K)
+  dt = mesh.cfl_dt()
+  sweep = pkg.ensemble.EnsembleSweep(mesh, ics, nsteps, dt)
+  partial = sweep.run().clone()
+  rows = host(sweep.per_ic())
+  signed = []
+  for j in ics:
+    op = pkg.operators.DGAdvection1D(mesh)
+    snaps = op.new_field(nsteps + 1)
+    op.init_sine(*pkg.ensemble.ic_params([j]), out=snaps[0])
+    op.forward(snaps[0], 0.0, dt, nsteps, snaps)
+    eta = torch.zeros(K, dtype=torch.float64, device=gpu)
+    op.adjoint(snaps[nsteps], snaps, 0.0, dt, nsteps, eta=eta)
+    torch.cuda.synchronize()
+    signed.append(host(eta))
+  signed = np.array(signed)
+  np.testing.assert_array_equal(rows, np.abs(signed))
+  np.testing.assert_array_equal(host(partial), oadj.sum_rows(np.abs(signed)))
+  mean, idx = pkg.ensemble.gather_indicator(partial, len(ics),
+                                            pkg.ensemble.DeviceReducer(sweep.op))
+  np.testing.assert_allclose(host(mean), oadj.ensemble_indicator(signed), rtol=1e-15)
+  assert int(idx[0]) == oadj.argmax(oadj.ensemble_indicator(signed), use_abs=True)
+
+
+def test_argmax_ex_value_and_nonfinite_count(pkg, gpu):
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=2, k=5000)
+  op = pkg.operators.DGAdvection1D(mesh)
+  rng = np.random.default_rng(3)
+  x = rng.standard_normal(5000)
+  x[[17, 4000]] = -9.5  # tie in |x|: first index wins
+  xd = torch.tensor(x, device=gpu)
+  idx = torch.zeros(1, dtype=torch.int64, device=gpu)
+  val = torch.zeros(1, dtype=torch.float64, device=gpu)
+  bad = torch.zeros(1, dtype=torch.int64, device=gpu)
+  op.argmax_ex(xd, idx, val, bad)
+  torch.cuda.synchronize()
+  assert int(idx) == 17 == oadj.argmax(x, use_abs=True)
+  assert float(val) == 9.5 and int(bad) == 0
+  op.argmax_ex(xd, idx, val, bad, use_abs=False)
+  assert int(idx) == int(np.argmax(x)) and float(val) == x.max()
+  for poison in (np.nan, np.inf, -np.inf):
+    y = x.copy()
+    y[2222] = poison
+    op.argmax_ex(torch.tensor(y, device=gpu), idx, val, bad)
+    torch.cuda.synchronize()
+    assert int(idx) == 2222
+  assert int(bad) == 3  # counted once per call that saw a non-finite winner
+
+
+@pytest.mark.parametrize("n", [1, 2, 1001, (1 << 22) + 3])
+def test_stream_copy_is_exact(pkg, gpu, n):
+  import torch
+  src = torch.randn(n, dtype=torch.float64, device=gpu)
+  dst = torch.zeros_like(src)
+  pkg.operators.stream_copy(src, dst)
+  torch.cuda.synchronize()
+  assert torch.equal(src, dst)
+
+
+def test_stream_copy_rejects_misaligned(pkg, gpu):
+  import torch
+  src = torch.randn(101, dtype=torch.float64, device=gpu)
+  dst = torch.zeros(101, dtype=torch.float64, device=gpu)
+  with pytest.raises(pkg._lib.DGLibraryError, match="aligned"):
+    pkg.operators.stream_copy(src[1:], dst[1:])
