@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdgadv.so")
+# DG_LIB_PATH: an experiment variant built by build_ext --out (A/B runs only); default: the
+# in-tree product library.
+LIB_PATH = os.environ.get("DG_LIB_PATH") or os.path.join(_HERE, "lib", "libdgadv.so")
 HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "include", "dg_advec.h"))
 
 # Enumerations of include/dg_advec.h
@@ -44,7 +46,9 @@ SIGNATURES = {
     "dg_lserk4_adj": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32,
                              ctypes.c_double, _vp, _vp]),
     "dg_lserk4_adj_ex": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32,
-                                ctypes.c_double, _vp, _i32, _vp]),
+                                ctypes.c_double, _vp, _i32, _vp, _vp]),
+    "dg_lserk4_fwd_ex": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp,
+                                _vp]),
     "dg_slope_limit_n": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dg_slope_limit_1": (_i32, [_vp, _vp, _vp, _vp]),
     "dg_argmax": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),

@@ -52,6 +52,9 @@ class AdaptiveSweep:
     self._snaps = torch.empty((self.nsteps + 1) * k_cap * mesh.n_p, dtype=torch.float64,
                               device=dev)
     self._eta = torch.zeros(k_cap, dtype=torch.float64, device=dev)
+    # the forward sweep's limiter decisions, read back by the adjoint (dg_lserk4_fwd_ex)
+    self._codes = (torch.zeros(self.nsteps * k_cap, dtype=torch.int16, device=dev)
+                   if self.op.limiter else None)
     self.idx = torch.zeros(1, dtype=torch.int64, device=dev)
     self.h_split = torch.zeros(1, dtype=torch.float64, device=dev)
     # min |x_1 - x_2| over elements = h_min * (r_1 - r_0) / 2 (LGL nodes are affine images)
@@ -77,26 +80,31 @@ class AdaptiveSweep:
     return self._eta[:self.op.ktot]
 
   def init_state(self):
-    """u^0 = the IC on the current mesh (snapshot 0) and eta = 0."""
+    """u^0 = the IC on the current mesh (snapshot 0).  (eta needs no reset: the adjoint's
+    first launch assigns it, DG_ADJ_ETA_ASSIGN.)"""
     amp, freq, phase = self.ic
     self.op.init_sine([amp], [freq], [phase], out=self.snapshots()[0])
-    self.eta().zero_()
+
+  def decisions(self):
+    return None if self._codes is None else self._codes[:self.nsteps * self.op.ktot]
 
   def forward(self, dt=None, init=True):
     """init_state() (unless init=False: the caller did it) then the forward sweep."""
     snaps = self.snapshots()
     if init:
       self.init_state()
-    self.op.forward(snaps[0], self.t0, self.dt if dt is None else dt, self.nsteps, snaps)
+    self.op.forward(snaps[0], self.t0, self.dt if dt is None else dt, self.nsteps, snaps,
+                    decisions=self.decisions())
     return snaps
 
   def adjoint(self, dt=None):
-    """The adjoint sweep accumulating into eta (zeroed by init_state)."""
+    """The adjoint sweep writing eta (assigned by its first launch), with the forward's
+    recorded limiter decisions."""
     snaps = self.snapshots()
     eta = self.eta()
     # J = |u^N|^2 / 2: the terminal adjoint is u^N itself; the sweep runs in place on it.
     self.op.adjoint(snaps[self.nsteps], snaps, self.t0, self.dt if dt is None else dt,
-                    self.nsteps, eta=eta)
+                    self.nsteps, eta=eta, eta_assign=True, decisions=self.decisions())
     return eta
 
   def refine(self):

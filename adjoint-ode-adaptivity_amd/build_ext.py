@@ -25,15 +25,19 @@ def hipcc():
   raise RuntimeError("hipcc not found (ROCm is required to build the HIP extension)")
 
 
-def build(force=False, verbose=True, extra_flags=()):
+def build(force=False, verbose=True, extra_flags=(), out=None):
+  """Build lib/libdgadv.so; `out` + `extra_flags` build an experiment variant elsewhere
+  (its own object directory; the product library is untouched)."""
+  OUT_ = OUT if out is None else os.path.abspath(out)
   deps = SRCS + [COMMON, os.path.join(INCLUDE, "dg_advec.h")]
-  if (not force and os.path.exists(OUT)
-      and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps)):
+  if (not force and os.path.exists(OUT_)
+      and os.path.getmtime(OUT_) >= max(os.path.getmtime(d) for d in deps)):
     if verbose:
-      print(f"[build_ext] up to date: {OUT}")
-    return OUT
-  os.makedirs(os.path.dirname(OUT), exist_ok=True)
-  objdir = os.path.join(os.path.dirname(OUT), "obj")
+      print(f"[build_ext] up to date: {OUT_}")
+    return OUT_
+  os.makedirs(os.path.dirname(OUT_), exist_ok=True)
+  objdir = os.path.join(os.path.dirname(OUT_), "obj" if out is None else
+                        "obj_" + os.path.basename(OUT_).replace(".so", ""))
   os.makedirs(objdir, exist_ok=True)
   flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-I", INCLUDE, *extra_flags]
   procs, objs = [], []
@@ -41,7 +45,7 @@ def build(force=False, verbose=True, extra_flags=()):
   for src in SRCS:
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
     objs.append(obj)
-    if (not force and not extra_flags and os.path.exists(obj)
+    if (not force and os.path.exists(obj)
         and os.path.getmtime(obj) >= max(os.path.getmtime(src), shared)):
       continue  # this translation unit is up to date
     cmd = [hipcc(), *flags, "-c", "-o", obj, src]
@@ -50,16 +54,22 @@ def build(force=False, verbose=True, extra_flags=()):
     procs.append((subprocess.Popen(cmd), src))
   failed = [src for p, src in procs if p.wait() != 0]
   if failed:
-    raise RuntimeError(f"hipcc failed on {failed}; {OUT} was NOT updated")
-  tmp = OUT + ".tmp"
+    raise RuntimeError(f"hipcc failed on {failed}; {OUT_} was NOT updated")
+  tmp = OUT_ + ".tmp"
   cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
   if verbose:
     print("[build_ext]", " ".join(cmd))
   if subprocess.run(cmd).returncode != 0:
-    raise RuntimeError(f"link failed; {OUT} was NOT updated")
-  os.replace(tmp, OUT)
-  return OUT
+    raise RuntimeError(f"link failed; {OUT_} was NOT updated")
+  os.replace(tmp, OUT_)
+  return OUT_
 
 
 if __name__ == "__main__":
-  build(force="--force" in sys.argv)
+  import argparse
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--force", action="store_true")
+  ap.add_argument("--out", default=None, help="variant library path (experiments)")
+  ap.add_argument("-D", action="append", default=[], help="extra -D defines")
+  a = ap.parse_args()
+  build(force=a.force, out=a.out, extra_flags=tuple("-D" + d for d in a.D))

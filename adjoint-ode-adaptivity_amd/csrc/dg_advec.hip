@@ -32,13 +32,13 @@ namespace {
 using namespace dgk;
 
 template <int NP, int NS, bool UNI, int W, int MS>
-__global__ __launch_bounds__(kBlock * W) void k_step(const double* __restrict__ uin,
+__global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* __restrict__ uin,
                                                      double* __restrict__ snap,
                                                      double* __restrict__ last,
                                                      const double* __restrict__ scale,
                                                      StepArgs<NP, NS, MS> args);
 template <int NP, int NS, bool UNI, int W, int MS>
-__global__ __launch_bounds__(kBlock * W) void k_adj(const double* __restrict__ win,
+__global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(const double* __restrict__ win,
                                                     double* __restrict__ wout,
                                                     const double* __restrict__ snap,
                                                     double* __restrict__ eta,
@@ -194,7 +194,7 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
 }
 
 template <int NP, int NS, bool UNI, int W, int MS>
-__global__ __launch_bounds__(kBlock * W) void k_step(const double* __restrict__ uin,
+__global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* __restrict__ uin,
                                                      double* __restrict__ snap,
                                                      double* __restrict__ last,
                                                      const double* __restrict__ scale,
@@ -414,7 +414,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 }
 
 template <int NP, int NS, bool UNI, int W, int MS>
-__global__ __launch_bounds__(kBlock * W) void k_adj(const double* __restrict__ win,
+__global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(const double* __restrict__ win,
                                                     double* __restrict__ wout,
                                                     const double* __restrict__ snap,
                                                     double* __restrict__ eta,
@@ -878,6 +878,7 @@ int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const 
 inline int effective_msteps(const dg_plan* p) {
   int m = p->msteps;
   if (m == 8 && !(p->tile_width == 2 || p->lane_elems == 8)) m = 4;
+  if (m == 8 && p->lane_elems == 2) m = 4;  // 128-element wave tiles: cone too wide
   if (p->NP > 8 && m > 2) m = 2;
   return m;
 }
@@ -958,9 +959,14 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   p->uniform = (hmax - hmin) <= 1e-12 * hmean;
   p->s_uniform = 2.0 / hmean;
 
-  // Per-N default shape (config 5 sweep, profiles/r01/tune/N*.json): 512-element tiles
-  // pay off at low order, where a lane's work per stage is small.
+  // Per-N default shape (config 5 sweeps, profiles/r01/tune/N*.json and
+  // profiles/r02/tune/): 512-element tiles pay off at low order, where a lane's work per
+  // stage is small; at N = 1 the forward runs on one-wave tiles of 4 elements per lane
+  // (DPP face exchange, no barriers: 23.8 -> 18.9 us per 4-step launch), at N = 2 both
+  // directions take 8 steps per launch (bench 3.82e11 -> 4.03e11 DOF-updates/s).
   p->tile_width = (N <= 2) ? 2 : 1;
+  if (N == 1) p->lane_elems = 4;
+  if (N == 2) p->msteps = 8;
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);
@@ -1146,6 +1152,11 @@ int dg_advec_rhs(const dg_plan* p, const double* u, double* rhs, double t, void*
 
 int dg_lserk4_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
                   void* stream) {
+  return dg_lserk4_fwd_ex(p, u, t0, dt, nsteps, snapshots, nullptr, stream);
+}
+
+int dg_lserk4_fwd_ex(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
+                     uint16_t* decisions, void* stream) {
   if (!p || !u) return fail(DG_ERR_ARG, "null argument");
   if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -1155,7 +1166,8 @@ int dg_lserk4_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, doubl
       HIP_TRY(hipMemcpyAsync(snapshots, u, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
     return DG_OK;
   }
-  if (p->nonlinear()) return nl_fwd(p, u, t0, dt, nsteps, snapshots, st);
+  if (p->nonlinear())
+    return nl_fwd(p, u, t0, dt, nsteps, snapshots, p->limiter ? decisions : nullptr, st);
   // Time levels by repeated addition (time = time + dt, One_code.mlx:139).
   std::vector<double> tn(size_t(nsteps) + 1);
   tn[0] = t0;
@@ -1195,18 +1207,21 @@ int dg_lserk4_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, doubl
 
 int dg_lserk4_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
                   int nsteps, double src_coef, double* eta, void* stream) {
-  return dg_lserk4_adj_ex(p, w, snapshots, t0, dt, nsteps, src_coef, eta, 0, stream);
+  return dg_lserk4_adj_ex(p, w, snapshots, t0, dt, nsteps, src_coef, eta, 0, nullptr, stream);
 }
 
 int dg_lserk4_adj_ex(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
-                     int nsteps, double src_coef, double* eta, int flags, void* stream) {
+                     int nsteps, double src_coef, double* eta, int flags,
+                     const uint16_t* decisions, void* stream) {
   if (!p || !w || !snapshots) return fail(DG_ERR_ARG, "null argument");
   if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
   if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS)) return fail(DG_ERR_ARG, "unknown flags");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (eta != nullptr && nsteps == 0 && (flags & DG_ADJ_ETA_ASSIGN))  // nothing to assign from
     HIP_TRY(hipMemsetAsync(eta, 0, sizeof(double) * p->ktot, st));
-  if (p->nonlinear()) return nl_adj(p, w, snapshots, t0, dt, nsteps, src_coef, eta, flags, st);
+  if (p->nonlinear())
+    return nl_adj(p, w, snapshots, t0, dt, nsteps, src_coef, eta, flags,
+                  p->limiter ? decisions : nullptr, st);
   const int64_t field = p->ktot * p->NP;
   // Same time levels as the forward sweep (repeated addition).
   std::vector<double> tn(size_t(nsteps) + 1), src(size_t(nsteps) + 1, src_coef);

@@ -89,8 +89,8 @@ __device__ __forceinline__ void flux_eo(const double* ev, const double* od, doub
 // Exchange arrays in LDS (doubles, each padded by one slot on the left): two
 // double-buffered face pairs [0, 4(T+2)), cell averages [4(T+2), 5(T+2)), the adjoint's
 // limiter contributions to the left / right neighbour [5(T+2), 7(T+2)).
-template <int NP> struct NLGeo {
-  static constexpr int T = kBlock;
+template <int NP, int W = 1> struct NLGeo {
+  static constexpr int T = kBlock * W;
   static constexpr int FA = 4 * (T + 2), CL = 5 * (T + 2), CR = 6 * (T + 2);
   static constexpr int kEx = 7 * (T + 2);
   static constexpr int kTileD = T * NP + 2;
@@ -99,15 +99,25 @@ template <int NP> struct NLGeo {
 
 // One LSERK4 stage s of the lane's element:  r = A_s r + dt RHS(u);  v = u + B_s r;
 // u = SlopeLimitN(v) if LIM.  Returns the limiter's decision: 0 if the cell is not
-// troubled, else 4 | (the active minmod argument, 0..3).  iin: LDS slot of the stage's
+// troubled, else 4 | (the active minmod argument, 1..3).  iin: LDS slot of the stage's
 // inflow flux f(uin).  Barriers: one (faces), two with the limiter (cell averages).
-template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE>
+//
+// Metric: the operator constants carry dt (and 2/h on uniform meshes).  On non-uniform
+// meshes the low-storage residual is kept divided by the element's 2/h = sc (r' = r / sc:
+// r' = A_s r' + dt L u), so the stage is the uniform one except for the update
+// v = u + (B_s sc) r' -- no per-node metric multiplies.
+//
+// KNOWN: the decisions come from the forward sweep's record `kc` (this stage's 3 bits)
+// instead of the troubled-cell test, and `any` (workgroup-uniform: some lane of the tile is
+// troubled in this stage) gates the cell-average exchange: a stage without a troubled cell
+// in the tile runs no limiter work and no second barrier.
+template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE, bool KNOWN, int W>
 __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s, int par, int iin,
                                         const Elem& E, double sc, const EOArgs<NP>& op,
                                         const LimEO<NP>& lc, double* ev, double* od,
-                                        double* re, double* ro) {
-  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, T = kBlock;
-  constexpr int FA = NLGeo<NP>::FA;
+                                        double* re, double* ro, int kc = 0, bool any = true) {
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, T = kBlock * W;
+  constexpr int FA = NLGeo<NP, W>::FA;
   // par: face buffer, alternating over consecutive stages (across steps too: without the
   // limiter no barrier separates a step's last face reads from the next step's writes)
   const int fL = par * 2 * (T + 2), fR = fL + (T + 2);
@@ -117,19 +127,19 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
   lds[fL + el + 1] = f0;
   lds[fR + el + 1] = fN;
   __builtin_amdgcn_sched_barrier(0);
-  double pe[NE], po[NO];  // volume term (+ the carry A_s r on uniform meshes)
+  double pe[NE], po[NO];  // volume term + the carry A_s r'
 #pragma unroll
   for (int k = 0; k < NE; ++k) {
-    double t = (UNI && s > 0) ? RK<5>::A(s) * re[k] : op.Qeo[k * NO] * fo[0];
+    double t = (s > 0) ? RK<5>::A(s) * re[k] : op.Qeo[k * NO] * fo[0];
 #pragma unroll
-    for (int j = (UNI && s > 0) ? 0 : 1; j < NO; ++j) t = fma(op.Qeo[k * NO + j], fo[j], t);
+    for (int j = (s > 0) ? 0 : 1; j < NO; ++j) t = fma(op.Qeo[k * NO + j], fo[j], t);
     pe[k] = t;
   }
 #pragma unroll
   for (int k = 0; k < NO; ++k) {
-    double t = (UNI && s > 0) ? RK<5>::A(s) * ro[k] : op.Qoe[k * NE] * fe[0];
+    double t = (s > 0) ? RK<5>::A(s) * ro[k] : op.Qoe[k * NE] * fe[0];
 #pragma unroll
-    for (int j = (UNI && s > 0) ? 0 : 1; j < NE; ++j) t = fma(op.Qoe[k * NE + j], fe[j], t);
+    for (int j = (s > 0) ? 0 : 1; j < NE; ++j) t = fma(op.Qoe[k * NE + j], fe[j], t);
     po[k] = t;
   }
 #pragma unroll
@@ -144,29 +154,23 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
   const double du0 = f0 - lds[iL];
   const double du1 = fN - lds[iR];
   const double dlt = du0 - du1, sig = du0 + du1;
+  const double bs = UNI ? RK<5>::B(s) : RK<5>::B(s) * sc;
 #pragma unroll
   for (int k = 0; k < NE; ++k) {
-    if constexpr (UNI) {
-      re[k] = fma(op.le[k], dlt, pe[k]);
-    } else {
-      const double a = sc * fma(op.le[k], dlt, pe[k]);
-      re[k] = (s == 0) ? a : fma(RK<5>::A(s), re[k], a);
-    }
-    ev[k] = fma(RK<5>::B(s), re[k], ev[k]);
+    re[k] = fma(op.le[k], dlt, pe[k]);
+    ev[k] = fma(bs, re[k], ev[k]);
   }
 #pragma unroll
   for (int k = 0; k < NO; ++k) {
-    if constexpr (UNI) {
-      ro[k] = fma(op.lo[k], sig, po[k]);
-    } else {
-      const double a = sc * fma(op.lo[k], sig, po[k]);
-      ro[k] = (s == 0) ? a : fma(RK<5>::A(s), ro[k], a);
-    }
-    od[k] = fma(RK<5>::B(s), ro[k], od[k]);
+    ro[k] = fma(op.lo[k], sig, po[k]);
+    od[k] = fma(bs, ro[k], od[k]);
   }
   if constexpr (!LIM) {
     return 0;
   } else {
+    if constexpr (KNOWN) {
+      if (!any) return 0;  // workgroup-uniform: no troubled cell in the tile this stage
+    }
     double avg = lc.a0e[0] * ev[0];
 #pragma unroll
     for (int k = 1; k < NE; ++k) avg = fma(lc.a0e[k], ev[k], avg);
@@ -175,12 +179,26 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
     // Neighbour averages, replicated at a trajectory's ends (SlopeLimitN.m:18).
     const double am = lds[EDGE && E.first ? FA + el + 1 : FA + el];
     const double ap = lds[EDGE && E.last ? FA + el + 1 : FA + el + 2];
-    if (!lc.every && !troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0])) return 0;
-    double uh1 = lc.a1o[0] * od[0];
-#pragma unroll
-    for (int k = 1; k < NO; ++k) uh1 = fma(lc.a1o[k], od[k], uh1);
+    double uh1 = 0.0;
     int br;
-    const double hm = minmod_br(fma(lc.dv0, avg, lc.dv1 * uh1), ap - avg, avg - am, br);
+    double hm;
+    if constexpr (KNOWN) {
+      if (!(kc & 4)) return 0;
+      uh1 = lc.a1o[0] * od[0];
+#pragma unroll
+      for (int k = 1; k < NO; ++k) uh1 = fma(lc.a1o[k], od[k], uh1);
+      // the recorded active minmod argument IS the minmod value (minmod.m:9-11: the
+      // argument of least magnitude, all arguments of one sign)
+      br = kc & 3;
+      const double a1 = fma(lc.dv0, avg, lc.dv1 * uh1);
+      hm = br == 1 ? a1 : (br == 2 ? ap - avg : (br == 3 ? avg - am : 0.0));
+    } else {
+      if (!lc.every && !troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0])) return 0;
+      uh1 = lc.a1o[0] * od[0];
+#pragma unroll
+      for (int k = 1; k < NO; ++k) uh1 = fma(lc.a1o[k], od[k], uh1);
+      hm = minmod_br(fma(lc.dv0, avg, lc.dv1 * uh1), ap - avg, avg - am, br);
+    }
 #pragma unroll
     for (int k = 0; k < NE; ++k) ev[k] = avg;
 #pragma unroll
@@ -191,10 +209,10 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
 
 // Interior elements [H, T-H) of the tile to LDS (element-major, nodal); dual = adjoint
 // coordinates (w_k = (we + wo)/2, w_{N-k} = (we - wo)/2).
-template <int NP, int H>
+template <int NP, int H, int W>
 __device__ __forceinline__ void put_interior(double* __restrict__ lds, const double* ev,
                                              const double* od, bool dual) {
-  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1, T = kBlock;
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1, T = kBlock * W;
   const int el = threadIdx.x;
   if (el >= H && el < T - H) {
     double* o = lds + (el - H) * NP;
@@ -227,11 +245,19 @@ template <int NP, int MS> struct NLStepArgs {
 
 template <bool LIM> constexpr int cone_per_stage() { return LIM ? 2 : 1; }
 
+// Tile widths of the config-3 kernels: workgroups of 256*W lanes own tiles of 256*W
+// elements.  Measured at K = 2^22 (bench.py --config 3): the forward (64 VGPRs, 8 waves per
+// SIMD) gains from 512-element tiles (halo 4 % instead of 8 %: 101 -> 93 us per step with the
+// SGPR cap); the adjoint (117 VGPRs, 4 waves per SIMD) loses (145 -> 151 us): with two
+// 8-wave workgroups per CU each barrier stalls half the CU's waves.
+constexpr int kNLStepW = 2, kNLAdjW = 1;
+
 template <int NP, bool BURG, bool LIM, bool UNI, int MS>
-__global__ __launch_bounds__(kBlock) void k_step_nl(const double* __restrict__ uin,
+__global__ __launch_bounds__(kBlock * kNLStepW) DG_NL_STEP_ATTR void k_step_nl(const double* __restrict__ uin,
                                                     double* __restrict__ snap,
                                                     double* __restrict__ last,
                                                     const double* __restrict__ scale,
+                                                    uint16_t* __restrict__ codes,
                                                     NLStepArgs<NP, MS> args);
 
 template <int NP, bool BURG, bool LIM, bool UNI, int MS, bool EDGE>
@@ -239,12 +265,13 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
                                              const double* __restrict__ uin,
                                              double* __restrict__ snap, double* __restrict__ last,
                                              const double* __restrict__ scale,
+                                             uint16_t* __restrict__ codes,
                                              const NLStepArgs<NP, MS>& args) {
-  constexpr int T = kBlock, NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
+  constexpr int W = kNLStepW, T = kBlock * W, NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
   constexpr int H = MS * 5 * cone_per_stage<LIM>();
   constexpr int TE = T - 2 * H;
   static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
-  constexpr int CB = NLGeo<NP>::kLds;  // lds[CB + st*5 + s] = inflow flux of that stage
+  constexpr int CB = NLGeo<NP, W>::kLds;  // lds[CB + st*5 + s] = inflow flux of that stage
   const int lane = threadIdx.x;
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
@@ -252,9 +279,9 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
   const int64_t rem = nd - o0;
   const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
 
-  TileRegs<NP, 1> pf;
-  tile_issue<NP, 1, EDGE>(uin, e0, nd, pf);
-  tile_commit<NP, 1>(pf, lds);
+  TileRegs<NP, W> pf;
+  tile_issue<NP, W, EDGE>(uin, e0, nd, pf);
+  tile_commit<NP, W>(pf, lds);
   if constexpr (EDGE) {
     // Lane-indexed read of fin straight from the kernel-argument segment (the args follow
     // the pointer arguments of k_step_nl; layout pinned by kernarg_tail), as in k_step.
@@ -275,13 +302,19 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
   double re[NE], ro[NO];
 #pragma unroll
   for (int st = 0; st < MS; ++st) {
+    int c15 = 0;  // this step's limiter decisions, 3 bits per stage
 #pragma unroll
     for (int s = 0; s < 5; ++s)
-      nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, (st * 5 + s) & 1, CB + st * 5 + s, E, sc,
-                                         args.op, args.lc, ev, od, re, ro);
+      c15 |= nl_stage<NP, BURG, LIM, UNI, EDGE, false, W>(lds, lane, s, (st * 5 + s) & 1,
+                                                          CB + st * 5 + s, E, sc, args.op, args.lc,
+                                                          ev, od, re, ro)
+             << (3 * s);
+    // The decision record for the adjoint (dg_lserk4_fwd_ex): one 16-bit word per element
+    // and step, written by the lane that owns the element.
+    if (LIM && codes != nullptr && E.valid) codes[st * args.ktot + E.e] = uint16_t(c15);
     if (snap != nullptr || st == MS - 1) {
       __syncthreads();  // the last stage's exchange reads are done before the image is rewritten
-      put_interior<NP, H>(lds, ev, od, false);
+      put_interior<NP, H, W>(lds, ev, od, false);
       __syncthreads();
       if constexpr (EDGE) {
         if (snap != nullptr) store_run<T>(snap + st * args.stride, o0, count, lds);
@@ -296,19 +329,20 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
 }
 
 template <int NP, bool BURG, bool LIM, bool UNI, int MS>
-__global__ __launch_bounds__(kBlock) void k_step_nl(const double* __restrict__ uin,
+__global__ __launch_bounds__(kBlock * kNLStepW) DG_NL_STEP_ATTR void k_step_nl(const double* __restrict__ uin,
                                                     double* __restrict__ snap,
                                                     double* __restrict__ last,
                                                     const double* __restrict__ scale,
+                                                    uint16_t* __restrict__ codes,
                                                     NLStepArgs<NP, MS> args) {
-  constexpr int T = kBlock, H = MS * 5 * cone_per_stage<LIM>();
-  __shared__ __attribute__((aligned(16))) double lds[NLGeo<NP>::kLds + MS * 5];
+  constexpr int T = kBlock * kNLStepW, H = MS * 5 * cone_per_stage<LIM>();
+  __shared__ __attribute__((aligned(16))) double lds[NLGeo<NP, kNLStepW>::kLds + MS * 5];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
   const int64_t e0 = tile * (T - 2 * H) - H;
   if (edge_tile(e0, T, args.ktot, args.K))
-    nl_step_tile<NP, BURG, LIM, UNI, MS, true>(lds, tile, uin, snap, last, scale, args);
+    nl_step_tile<NP, BURG, LIM, UNI, MS, true>(lds, tile, uin, snap, last, scale, codes, args);
   else
-    nl_step_tile<NP, BURG, LIM, UNI, MS, false>(lds, tile, uin, snap, last, scale, args);
+    nl_step_tile<NP, BURG, LIM, UNI, MS, false>(lds, tile, uin, snap, last, scale, codes, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -326,41 +360,44 @@ template <int NP> struct NLAdjArgs {
   int32_t xcd;
 };
 
-template <int NP, bool BURG, bool LIM, bool UNI>
-__global__ __launch_bounds__(kBlock) void k_adj_nl(const double* __restrict__ win,
+template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN>
+__global__ __launch_bounds__(kBlock * kNLAdjW, DG_NL_ADJ_MINW) DG_NL_SGPR_ATTR void k_adj_nl(const double* __restrict__ win,
                                                    double* __restrict__ wout,
                                                    const double* __restrict__ snap,
                                                    double* __restrict__ eta,
                                                    const double* __restrict__ scale,
+                                                   const uint16_t* __restrict__ codes,
                                                    NLAdjArgs<NP> args);
 
-template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE>
+template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN, bool EDGE>
 __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t tile,
                                             const double* __restrict__ win,
                                             double* __restrict__ wout,
                                             const double* __restrict__ snap,
                                             double* __restrict__ eta,
                                             const double* __restrict__ scale,
+                                            const uint16_t* __restrict__ codes,
                                             const NLAdjArgs<NP>& args) {
-  constexpr int T = kBlock, NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  constexpr int W = kNLAdjW, T = kBlock * W, NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   // forward recompute and reverse sweep each widen the cone by one stage-cone per stage
   constexpr int H = 10 * cone_per_stage<LIM>();
   constexpr int TE = T - 2 * H;
   static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
-  constexpr int CB = NLGeo<NP>::kLds;  // lds[CB+s]: stage inflow flux; CB+5: residual's; CB+6: 0
-  constexpr int CL = NLGeo<NP>::CL, CR = NLGeo<NP>::CR;
+  constexpr int CB = NLGeo<NP, W>::kLds;  // lds[CB+s]: stage inflow flux; CB+5: residual's; CB+6: 0
+  constexpr int CL = NLGeo<NP, W>::CL, CR = NLGeo<NP, W>::CR;
   const int lane = threadIdx.x;
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
-  TileRegs<NP, 1> pu, pw;
-  tile_issue<NP, 1, EDGE>(snap, e0, nd, pu);
-  tile_issue<NP, 1, EDGE>(win, e0, nd, pw);
-  tile_commit<NP, 1>(pu, lds);
+  TileRegs<NP, W> pu, pw;
+  tile_issue<NP, W, EDGE>(snap, e0, nd, pu);
+  tile_issue<NP, W, EDGE>(win, e0, nd, pw);
+  tile_commit<NP, W>(pu, lds);
   if constexpr (EDGE) {
     using AArgs = NLAdjArgs<NP>;  // the args follow the pointer arguments of k_adj_nl
     const double* ka = reinterpret_cast<const double*>(
-        kernarg_tail<decltype(&k_adj_nl<NP, BURG, LIM, UNI>), AArgs>() + offsetof(AArgs, fin));
+        kernarg_tail<decltype(&k_adj_nl<NP, BURG, LIM, UNI, KNOWN>), AArgs>() +
+        offsetof(AArgs, fin));
     if (lane < 6) lds[CB + lane] = ka[lane];
     if (lane == 6) lds[CB + 6] = 0.0;
   }
@@ -368,7 +405,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   double ev[NE], od[NO];
   to_eo<NP>(lds + pu.off + lane * NP, ev, od);
   __syncthreads();
-  tile_commit<NP, 1>(pw, lds);
+  tile_commit<NP, W>(pw, lds);
   __syncthreads();
   double we[NE], wo[NO];  // the adjoint in dual even/odd coordinates
   {
@@ -386,19 +423,46 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   __syncthreads();  // the exchange arrays alias the staging image
 
   // 1. Recompute the step's stages, keeping each stage's input and limiter decision.
+  //    KNOWN: the decisions are the forward sweep's record; `wg` (the OR over the tile's
+  //    lanes) says in which stages some cell of the tile is troubled at all -- in the
+  //    others the limiter and its exchange are skipped, here and in the reverse pass.
+  int kcode = 0, wg = 0;
+  if constexpr (KNOWN) {
+    // bitwise OR of the tile's records (__syncthreads_or would only say "some nonzero")
+    __shared__ int wg_or;
+    kcode = E.inrange ? int(codes[E.e]) : 0;
+    if (lane == 0) wg_or = 0;
+    __syncthreads();
+    if (kcode != 0) atomicOr(&wg_or, kcode);  // LDS atomic, rare lanes only
+    __syncthreads();
+    wg = wg_or;
+  }
+  // The stage inputs u_s feed the Burgers flux Jacobian of the reverse pass.  Registers
+  // hold u_2..u_4; u_1 goes to a lane-private LDS slot and u_0 = u^n is re-read from the
+  // snapshot (L2-resident) at the end: 20 VGPRs fewer at the peak (5 waves per SIMD
+  // instead of 4).
+  constexpr int SE1 = CB + 8;  // lds[SE1 + k*T + lane]: u_1 in even/odd coordinates
   double se[5][NE], so[5][NO];
-  int codes = 0;
+  int dcodes = 0;
   {
     double re[NE], ro[NO];
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
+      if (s >= 2) {
 #pragma unroll
-      for (int k = 0; k < NE; ++k) se[s][k] = ev[k];
+        for (int k = 0; k < NE; ++k) se[s][k] = ev[k];
 #pragma unroll
-      for (int k = 0; k < NO; ++k) so[s][k] = od[k];
-      const int c = nl_stage<NP, BURG, LIM, UNI, EDGE>(lds, lane, s, s & 1, CB + s, E, sc, args.op,
-                                                       args.lc, ev, od, re, ro);
-      if constexpr (LIM) codes |= c << (3 * s);
+        for (int k = 0; k < NO; ++k) so[s][k] = od[k];
+      } else if (BURG && s == 1) {
+#pragma unroll
+        for (int k = 0; k < NE; ++k) lds[SE1 + k * T + lane] = ev[k];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) lds[SE1 + (NE + k) * T + lane] = od[k];
+      }
+      const int c = nl_stage<NP, BURG, LIM, UNI, EDGE, KNOWN, W>(
+          lds, lane, s, s & 1, CB + s, E, sc, args.op, args.lc, ev, od, re, ro,
+          (kcode >> (3 * s)) & 7, ((wg >> (3 * s)) & 4) != 0);
+      if constexpr (LIM) dcodes |= c << (3 * s);
     }
   }
   // (ev, od) = u^{n+1}.  2. Functional source w^{n+1} += src u^{n+1} (dual coordinates).
@@ -443,13 +507,13 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 #pragma unroll
   for (int ss = 0; ss < 5; ++ss) {
     const int s = 4 - ss;
-    if constexpr (LIM) {
+    if (LIM && (!KNOWN || ((wg >> (3 * s)) & 4))) {  // (workgroup-uniform)
       // Transposed limiter.  Troubled cell: y = v_avg + (r/2) hm, hm one of
       // {2 (Dr V)(1,:) uh(1:2), v+ - v, v - v-} (or 0): the cell's own nodal adjoint is
       // replaced by the branch-1 gradient, and avg-adjoints go to this cell (cs) and to the
       // left / right neighbour (cl / cr).  Every cell then adds the avg-adjoint it
       // receives times d avg / d v.
-      const int code = (codes >> (3 * s)) & 7;
+      const int code = (dcodes >> (3 * s)) & 7;
       double cs = 0.0, cl = 0.0, cr = 0.0;
       if (code & 4) {
         double ls = we[0];
@@ -488,16 +552,18 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     const int f0 = (ss & 1) * 2 * (T + 2), f1 = f0 + (T + 2);
     double qe[NE], qo[NO];
     double gd = 0.0, gs = 0.0;
+    // transpose of v = u + (B_s sc) r' (nl_stage's metric folding): lr' += (B_s sc) lv
+    const double bs = UNI ? RK<5>::B(s) : RK<5>::B(s) * sc;
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
-      lre[k] = fma(RK<5>::B(s), we[k], lre[k]);
-      qe[k] = UNI ? lre[k] : sc * lre[k];
+      lre[k] = fma(bs, we[k], lre[k]);
+      qe[k] = lre[k];
       gd = fma(args.op.le[k], qe[k], gd);
     }
 #pragma unroll
     for (int k = 0; k < NO; ++k) {
-      lro[k] = fma(RK<5>::B(s), wo[k], lro[k]);
-      qo[k] = UNI ? lro[k] : sc * lro[k];
+      lro[k] = fma(bs, wo[k], lro[k]);
+      qo[k] = lro[k];
       gs = fma(args.op.lo[k], qo[k], gs);
     }
     const double g0 = gd + gs;  // adjoints of du0 and du1
@@ -535,13 +601,30 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     pe[0] += (g0 + g1) - (gr + gl);
     po[0] += (g0 - g1) + (gr - gl);
     if constexpr (BURG) {  // f'(u) = u: the symmetric block [[e, o], [o, e]] per node pair
+      double ue[NE], uo[NO];  // u_s (see the recompute)
+      if (s >= 2) {
+#pragma unroll
+        for (int k = 0; k < NE; ++k) ue[k] = se[s][k];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) uo[k] = so[s][k];
+      } else if (s == 1) {
+#pragma unroll
+        for (int k = 0; k < NE; ++k) ue[k] = lds[SE1 + k * T + lane];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) uo[k] = lds[SE1 + (NE + k) * T + lane];
+      } else {
+        double un[NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) un[i] = E.inrange ? snap[E.e * NP + i] : 0.0;
+        to_eo<NP>(un, ue, uo);
+      }
 #pragma unroll
       for (int k = 0; k < NO; ++k) {
-        const double e = se[s][k], o = so[s][k];
+        const double e = ue[k], o = uo[k];
         we[k] = fma(e, pe[k], fma(o, po[k], we[k]));
         wo[k] = fma(o, pe[k], fma(e, po[k], wo[k]));
       }
-      if constexpr (NE > NO) we[NO] = fma(se[s][NO], pe[NO], we[NO]);
+      if constexpr (NE > NO) we[NO] = fma(ue[NO], pe[NO], we[NO]);
     } else {
 #pragma unroll
       for (int k = 0; k < NE; ++k) we[k] += pe[k];
@@ -552,7 +635,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 
   if (args.has_eta && E.valid) eta_update(eta, E.e, eacc, args.has_eta);
   __syncthreads();  // the last stage's face reads are done before the image is rewritten
-  put_interior<NP, H>(lds, we, wo, true);
+  put_interior<NP, H, W>(lds, we, wo, true);
   __syncthreads();
   const int64_t o0 = tile * TE * NP;
   if constexpr (EDGE) {
@@ -563,21 +646,26 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   }
 }
 
-template <int NP, bool BURG, bool LIM, bool UNI>
-__global__ __launch_bounds__(kBlock) void k_adj_nl(const double* __restrict__ win,
+template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN>
+__global__ __launch_bounds__(kBlock * kNLAdjW, DG_NL_ADJ_MINW) DG_NL_SGPR_ATTR void k_adj_nl(const double* __restrict__ win,
                                                    double* __restrict__ wout,
                                                    const double* __restrict__ snap,
                                                    double* __restrict__ eta,
                                                    const double* __restrict__ scale,
+                                                   const uint16_t* __restrict__ codes,
                                                    NLAdjArgs<NP> args) {
-  constexpr int T = kBlock, H = 10 * cone_per_stage<LIM>();
-  __shared__ __attribute__((aligned(16))) double lds[NLGeo<NP>::kLds + 7];
+  constexpr int T = kBlock * kNLAdjW, H = 10 * cone_per_stage<LIM>();
+  // boundary constants (8 slots), then the lane-private stage-1 input (Burgers only)
+  __shared__ __attribute__((aligned(16)))
+  double lds[NLGeo<NP, kNLAdjW>::kLds + 8 + (BURG ? T * NP : 0)];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
   const int64_t e0 = tile * (T - 2 * H) - H;
   if (edge_tile(e0, T, args.ktot, args.K))
-    nl_adj_tile<NP, BURG, LIM, UNI, true>(lds, tile, win, wout, snap, eta, scale, args);
+    nl_adj_tile<NP, BURG, LIM, UNI, KNOWN, true>(lds, tile, win, wout, snap, eta, scale, codes,
+                                                 args);
   else
-    nl_adj_tile<NP, BURG, LIM, UNI, false>(lds, tile, win, wout, snap, eta, scale, args);
+    nl_adj_tile<NP, BURG, LIM, UNI, KNOWN, false>(lds, tile, win, wout, snap, eta, scale, codes,
+                                                  args);
 }
 
 // ---------------------------------------------------------------------------
@@ -661,11 +749,13 @@ inline double flux_value(bool burg, double u) { return burg ? 0.5 * u * u : u; }
 
 template <int NP, bool BURG, bool LIM, int MS>
 int launch_step_nl(const dg_plan* p, const double* in, double* snap, double* last,
-                   const double* times, double dt, hipStream_t st) {
+                   uint16_t* codes, const double* times, double dt, hipStream_t st) {
   NLStepArgs<NP, MS> a;
-  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  // constants carry dt (and 2/h on uniform meshes); non-uniform meshes multiply the update
+  // by the element's 2/h (nl_stage's metric folding)
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : dt, &a.op);
   a.lc = make_lim_eo<NP>(p);
-  a.sc = dt;
+  a.sc = 1.0;
   for (int m = 0; m < MS; ++m)
     for (int s = 0; s < 5; ++s)
       a.fin[m * 5 + s] = flux_value(BURG, inflow_value(p, times[m] + RK<5>::C(s) * dt));
@@ -673,25 +763,26 @@ int launch_step_nl(const dg_plan* p, const double* in, double* snap, double* las
   a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
   a.xcd = p->xcd_order;
-  constexpr int TE = kBlock - 2 * MS * 5 * cone_per_stage<LIM>();
+  constexpr int TE = kBlock * kNLStepW - 2 * MS * 5 * cone_per_stage<LIM>();
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_step_nl<NP, BURG, LIM, true, MS>), dim3(grid), dim3(kBlock), 0, st, in,
-                       snap, last, p->d_scale, a);
+    hipLaunchKernelGGL((k_step_nl<NP, BURG, LIM, true, MS>), dim3(grid), dim3(kBlock * kNLStepW), 0, st, in,
+                       snap, last, p->d_scale, codes, a);
   else
-    hipLaunchKernelGGL((k_step_nl<NP, BURG, LIM, false, MS>), dim3(grid), dim3(kBlock), 0, st,
-                       in, snap, last, p->d_scale, a);
+    hipLaunchKernelGGL((k_step_nl<NP, BURG, LIM, false, MS>), dim3(grid), dim3(kBlock * kNLStepW), 0, st,
+                       in, snap, last, p->d_scale, codes, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
 template <int NP, bool BURG, bool LIM>
 int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const double* snap,
-                  double* eta, int em, double t_n, double src, double dt, hipStream_t st) {
+                  double* eta, int em, const uint16_t* codes, double t_n, double src, double dt,
+                  hipStream_t st) {
   NLAdjArgs<NP> a;
-  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op);
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : dt, &a.op);  // see launch_step_nl
   a.lc = make_lim_eo<NP>(p);
-  a.sc = dt;
+  a.sc = 1.0;
   for (int s = 0; s < 5; ++s) a.fin[s] = flux_value(BURG, inflow_value(p, t_n + RK<5>::C(s) * dt));
   a.fin[5] = flux_value(BURG, inflow_value(p, t_n + dt));
   a.src = src;
@@ -699,14 +790,22 @@ int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const doubl
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr ? (em | kEtaOn) : 0;
   a.xcd = p->xcd_order;
-  constexpr int TE = kBlock - 20 * cone_per_stage<LIM>();
+  constexpr int TE = kBlock * kNLAdjW - 20 * cone_per_stage<LIM>();
   const unsigned grid = grid_for(p->ktot, TE);
-  if (p->uniform)
-    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, true>), dim3(grid), dim3(kBlock), 0, st, win,
-                       wout, snap, eta, p->d_scale, a);
+  // the recorded decisions are only kept with a limiter (without one there are none)
+  const bool known = LIM && codes != nullptr;
+  if (p->uniform && known)
+    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, true, true>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
+                       win, wout, snap, eta, p->d_scale, codes, a);
+  else if (p->uniform)
+    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, true, false>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
+                       win, wout, snap, eta, p->d_scale, codes, a);
+  else if (known)
+    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, false, true>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
+                       win, wout, snap, eta, p->d_scale, codes, a);
   else
-    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, false>), dim3(grid), dim3(kBlock), 0, st, win,
-                       wout, snap, eta, p->d_scale, a);
+    hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, false, false>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
+                       win, wout, snap, eta, p->d_scale, codes, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
@@ -715,32 +814,33 @@ int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const doubl
 // plain linear flux runs the k_step / k_adj kernels of dg_advec.hip).
 template <int NP>
 int step_np(const dg_plan* p, int ms, const double* in, double* snap, double* last,
-            const double* times, double dt, hipStream_t st) {
+            uint16_t* codes, const double* times, double dt, hipStream_t st) {
   const bool burg = p->flux == DG_FLUX_BURGERS, lim = p->limiter != 0;
   if (burg && lim)
-    return ms == 2 ? launch_step_nl<NP, true, true, 2>(p, in, snap, last, times, dt, st)
-                   : launch_step_nl<NP, true, true, 1>(p, in, snap, last, times, dt, st);
+    return ms == 2 ? launch_step_nl<NP, true, true, 2>(p, in, snap, last, codes, times, dt, st)
+                   : launch_step_nl<NP, true, true, 1>(p, in, snap, last, codes, times, dt, st);
   if (burg)
-    return ms == 2 ? launch_step_nl<NP, true, false, 2>(p, in, snap, last, times, dt, st)
-                   : launch_step_nl<NP, true, false, 1>(p, in, snap, last, times, dt, st);
-  return ms == 2 ? launch_step_nl<NP, false, true, 2>(p, in, snap, last, times, dt, st)
-                 : launch_step_nl<NP, false, true, 1>(p, in, snap, last, times, dt, st);
+    return ms == 2 ? launch_step_nl<NP, true, false, 2>(p, in, snap, last, codes, times, dt, st)
+                   : launch_step_nl<NP, true, false, 1>(p, in, snap, last, codes, times, dt, st);
+  return ms == 2 ? launch_step_nl<NP, false, true, 2>(p, in, snap, last, codes, times, dt, st)
+                 : launch_step_nl<NP, false, true, 1>(p, in, snap, last, codes, times, dt, st);
 }
 
 template <int NP>
 int adj_np(const dg_plan* p, const double* win, double* wout, const double* snap, double* eta,
-           int em, double t_n, double src, double dt, hipStream_t st) {
+           int em, const uint16_t* codes, double t_n, double src, double dt, hipStream_t st) {
   const bool burg = p->flux == DG_FLUX_BURGERS, lim = p->limiter != 0;
   if (burg && lim)
-    return launch_adj_nl<NP, true, true>(p, win, wout, snap, eta, em, t_n, src, dt, st);
-  if (burg) return launch_adj_nl<NP, true, false>(p, win, wout, snap, eta, em, t_n, src, dt, st);
-  return launch_adj_nl<NP, false, true>(p, win, wout, snap, eta, em, t_n, src, dt, st);
+    return launch_adj_nl<NP, true, true>(p, win, wout, snap, eta, em, codes, t_n, src, dt, st);
+  if (burg)
+    return launch_adj_nl<NP, true, false>(p, win, wout, snap, eta, em, codes, t_n, src, dt, st);
+  return launch_adj_nl<NP, false, true>(p, win, wout, snap, eta, em, codes, t_n, src, dt, st);
 }
 
 int launch_nl_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
-                   const double* times, double dt, hipStream_t st) {
+                   uint16_t* codes, const double* times, double dt, hipStream_t st) {
   int rc = DG_OK;
-  DG_DISPATCH_NP(p->NP, rc = step_np<NP>(p, ms, in, snap, last, times, dt, st));
+  DG_DISPATCH_NP(p->NP, rc = step_np<NP>(p, ms, in, snap, last, codes, times, dt, st));
   return rc;
 }
 
@@ -771,7 +871,7 @@ int nl_rhs(const dg_plan* p, const double* u, double* rhs, double t, hipStream_t
 }
 
 int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
-           hipStream_t st) {
+           uint16_t* decisions, hipStream_t st) {
   const int64_t field = p->ktot * p->NP;
   std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt (One_code.mlx:139)
   tn[0] = t0;
@@ -782,8 +882,10 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
     for (int n = 0; n < nsteps;) {
       const int m = chunk_nl(p, nsteps - n, true);
       double* last = (n + m == nsteps && snapshots != u) ? u : nullptr;
+      uint16_t* dec = decisions ? decisions + int64_t(n) * p->ktot : nullptr;
       const int rc = launch_nl_step(p, m, snapshots + int64_t(n) * field,
-                                    snapshots + int64_t(n + 1) * field, last, &tn[n], dt, st);
+                                    snapshots + int64_t(n + 1) * field, last, dec, &tn[n], dt,
+                                    st);
       if (rc) return rc;
       n += m;
     }
@@ -799,7 +901,8 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
   }
   for (int n = 0; n < nsteps;) {
     const int m = chunk_nl(p, nsteps - n, false);
-    const int rc = launch_nl_step(p, m, a, nullptr, b, &tn[n], dt, st);
+    uint16_t* dec = decisions ? decisions + int64_t(n) * p->ktot : nullptr;
+    const int rc = launch_nl_step(p, m, a, nullptr, b, dec, &tn[n], dt, st);
     if (rc) return rc;
     std::swap(a, b);
     n += m;
@@ -808,7 +911,7 @@ int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snap
 }
 
 int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,
-           double src_coef, double* eta, int flags, hipStream_t st) {
+           double src_coef, double* eta, int flags, const uint16_t* decisions, hipStream_t st) {
   const int64_t field = p->ktot * p->NP;
   std::vector<double> tn(size_t(nsteps) + 1);
   tn[0] = t0;
@@ -825,8 +928,9 @@ int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
     const int em = ((l == 0 && (flags & DG_ADJ_ETA_ASSIGN)) ? kEtaAssign : 0) |
                    ((n == 0 && (flags & DG_ADJ_ETA_ABS)) ? kEtaAbs : 0);
     int rc = DG_OK;
+    const uint16_t* dec = decisions ? decisions + int64_t(n) * p->ktot : nullptr;
     DG_DISPATCH_NP(p->NP, rc = adj_np<NP>(p, in, out, snapshots + int64_t(n) * field, eta, em,
-                                          tn[n], src, dt, st));
+                                          dec, tn[n], src, dt, st));
     if (rc) return rc;
     in = out;
   }

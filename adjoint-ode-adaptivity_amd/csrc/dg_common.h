@@ -25,6 +25,31 @@ constexpr int kBlock = 256;       // lanes per workgroup = elements per tile (in
 constexpr int kMaxNP = 9;         // N <= 8
 constexpr int kArgmaxParts = 1024;
 
+// SGPR budget of the hot step kernels.  The hardware admits 256-thread workgroups per CU up
+// to floor(800 / (ceil(sgpr/16)*16 + 16)) (MI355X_MICROARCH.md, Residency): 8 at <= 80
+// SGPRs, 7 at 82-96.  DG_SGPR_CAP caps the compiler's allocation (experiment knob).
+#ifdef DG_SGPR_CAP
+#define DG_SGPR_ATTR __attribute__((amdgpu_num_sgpr(DG_SGPR_CAP)))
+#else
+#define DG_SGPR_ATTR
+#endif
+#ifndef DG_ADJ_MINW
+#define DG_ADJ_MINW 1
+#endif
+// The same for the config-3 kernels, and the minimum waves per SIMD k_adj_nl's register
+// allocation targets (experiment knobs).
+#ifdef DG_NL_SGPR_CAP
+#define DG_NL_SGPR_ATTR __attribute__((amdgpu_num_sgpr(DG_NL_SGPR_CAP)))
+#else
+#define DG_NL_SGPR_ATTR
+#endif
+// k_step_nl: capped at 80 SGPRs so 8 workgroups fit per CU (at 94-100 SGPRs the hardware
+// admits 6-7; the spills go to VGPR lanes, the kernel stays at <= 64 VGPRs).
+#define DG_NL_STEP_ATTR __attribute__((amdgpu_num_sgpr(80)))
+#ifndef DG_NL_ADJ_MINW
+#define DG_NL_ADJ_MINW 5  // k_adj_nl: <= 96 VGPRs, 5 waves per SIMD (dg_burgers.hip)
+#endif
+
 // Indicator write mode of the adjoint kernels (the `has_eta` argument field):
 // bit 0 an indicator is wanted; bit 1 this launch assigns eta instead of adding to it (the
 // sweep's first launch under DG_ADJ_ETA_ASSIGN: no zero fill); bit 2 this launch stores
@@ -522,9 +547,9 @@ inline unsigned grid_for(int64_t n, int64_t per) { return unsigned((n + per - 1)
 // when plan->nonlinear().
 int nl_rhs(const dg_plan* p, const double* u, double* rhs, double t, hipStream_t st);
 int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
-           hipStream_t st);
+           uint16_t* decisions, hipStream_t st);
 int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,
-           double src_coef, double* eta, int flags, hipStream_t st);
+           double src_coef, double* eta, int flags, const uint16_t* decisions, hipStream_t st);
 
 // Wave-tile variants of the linear LSERK4 step kernels (dg_wave.hip), selected by
 // plan->lane_elems; `times` as for the workgroup-tile launchers.

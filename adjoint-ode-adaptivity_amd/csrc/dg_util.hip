@@ -5,7 +5,10 @@
 namespace {
 using namespace dgk;
 
-constexpr int kCopyVec = 4;  // 16-byte accesses per lane, all loads issued before the stores
+// 16-byte accesses per lane.  Measured on the box (profiles/probes/copy_probe.hip, 1 GiB):
+// 1 per lane 6.25 TB/s, 2 5.7, 4 5.4, 8 4.0; a grid-stride persistent grid 5.1; hipMemcpy
+// 4.5.  One access per lane and many small workgroups keep the most bytes in flight.
+constexpr int kCopyVec = 1;
 
 // dst = src, 16 bytes per lane per access.  Workgroup b owns the contiguous 16 KiB run
 // [b*kCopyVec*kBlock, (b+1)*kCopyVec*kBlock) of double2: each of its kCopyVec wave-loads is a

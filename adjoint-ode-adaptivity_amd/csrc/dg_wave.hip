@@ -246,13 +246,18 @@ int wstep_np(const dg_plan* p, int ms, const double* in, double* snap, double* l
     return launch_wstep_e<NP, 8, 1>(p, in, snap, last, times, dt, st);
   }
   if (p->lane_elems == 4) {
+    if (ms == 8) return launch_wstep_e<NP, 4, 8>(p, in, snap, last, times, dt, st);
     if (ms == 4) return launch_wstep_e<NP, 4, 4>(p, in, snap, last, times, dt, st);
     if (ms == 2) return launch_wstep_e<NP, 4, 2>(p, in, snap, last, times, dt, st);
-    return launch_wstep_e<NP, 4, 1>(p, in, snap, last, times, dt, st);
+    if (ms == 1) return launch_wstep_e<NP, 4, 1>(p, in, snap, last, times, dt, st);
+    return fail(DG_ERR_ARG, "wave tiles: unsupported steps per launch");
   }
+  // 2 elements per lane: a 128-element tile leaves no room for the 8-step cone
+  // (effective_msteps caps these plans at 4)
   if (ms == 4) return launch_wstep_e<NP, 2, 4>(p, in, snap, last, times, dt, st);
   if (ms == 2) return launch_wstep_e<NP, 2, 2>(p, in, snap, last, times, dt, st);
-  return launch_wstep_e<NP, 2, 1>(p, in, snap, last, times, dt, st);
+  if (ms == 1) return launch_wstep_e<NP, 2, 1>(p, in, snap, last, times, dt, st);
+  return fail(DG_ERR_ARG, "wave tiles of 2 elements per lane take at most 4 steps per launch");
 }
 
 }  // namespace

@@ -203,32 +203,48 @@ class DGAdvection1D:
     _lib.check(rc, "dg_advec_rhs")
     return out
 
-  def forward(self, u, t0, dt, nsteps, snapshots=None):
+  def _decisions(self, decisions, nsteps):
+    if decisions is None:
+      return None
+    if (not isinstance(decisions, torch.Tensor) or not decisions.is_cuda
+        or decisions.dtype != torch.int16 or not decisions.is_contiguous()):
+      raise TypeError("decisions must be a contiguous CUDA int16 tensor (uint16 bits)")
+    if decisions.numel() < nsteps * self.ktot:
+      raise ValueError(f"decisions holds {decisions.numel()} words, need {nsteps * self.ktot}")
+    return ctypes.c_void_p(decisions.data_ptr())
+
+  def forward(self, u, t0, dt, nsteps, snapshots=None, decisions=None):
     """nsteps fused steps in place on u (One_code.mlx:119-140); optional snapshots
-    ((nsteps+1) * field) receive u^0..u^nsteps."""
+    ((nsteps+1) * field) receive u^0..u^nsteps.  ``decisions`` (CUDA int16, nsteps*batch*K;
+    plans with a per-stage limiter) records the limiter's per-stage decisions for
+    ``adjoint`` (dg_lserk4_fwd_ex)."""
     snap_p = None
     if snapshots is not None:
       snap_p = self._field(snapshots, "snapshots", (nsteps + 1) * self.field_numel)
-    rc = self._lib.dg_lserk4_fwd(self._plan, self._field(u, "u"), float(t0), float(dt),
-                                 int(nsteps), snap_p, _stream(self.device))
-    _lib.check(rc, "dg_lserk4_fwd")
+    rc = self._lib.dg_lserk4_fwd_ex(self._plan, self._field(u, "u"), float(t0), float(dt),
+                                    int(nsteps), snap_p, self._decisions(decisions, nsteps),
+                                    _stream(self.device))
+    _lib.check(rc, "dg_lserk4_fwd_ex")
     return u
 
   def adjoint(self, w, snapshots, t0, dt, nsteps, src_coef=0.0, eta=None, eta_assign=False,
-              eta_abs=False):
+              eta_abs=False, decisions=None):
     """Discrete adjoint sweep in place on w (terminal dJ/du^N in, dJ/du^0 out) and the
     dual-weighted residual accumulated into eta (batch*K, caller-zeroed).
 
     ``eta_assign``: eta is assigned instead of accumulated (no zero fill needed);
     ``eta_abs``: eta ends as |eta| (Main_width_ref.py:139 ``jnp.abs(err)``).  Both are
-    folded into the sweep's first / last launch (dg_lserk4_adj_ex)."""
+    folded into the sweep's first / last launch (dg_lserk4_adj_ex).  ``decisions``: the
+    record ``forward`` wrote for these snapshots (limited plans): the frozen limiter
+    decisions are read instead of re-tested (bit-identical results, less work)."""
     eta_p = None if eta is None else self._field(eta, "eta", self.ktot)
     flags = (_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) | (_lib.DG_ADJ_ETA_ABS if eta_abs else 0)
     rc = self._lib.dg_lserk4_adj_ex(self._plan, self._field(w, "w"),
                                     self._field(snapshots, "snapshots",
                                                 (nsteps + 1) * self.field_numel),
                                     float(t0), float(dt), int(nsteps), float(src_coef), eta_p,
-                                    int(flags), _stream(self.device))
+                                    int(flags), self._decisions(decisions, nsteps),
+                                    _stream(self.device))
     _lib.check(rc, "dg_lserk4_adj_ex")
     return w, eta
 

@@ -141,6 +141,14 @@ int dg_advec_rhs(const dg_plan* plan, const double* u, double* rhs, double t, vo
 int dg_lserk4_fwd(dg_plan* plan, double* u, double t0, double dt, int nsteps,
                   double* snapshots, void* stream);
 
+/* dg_lserk4_fwd that also records the per-stage limiter's decisions (plans with a per-stage
+ * limiter only; ignored otherwise): decisions (nullable, device, nsteps*batch*K uint16) gets,
+ * for step n and element e, decisions[n*batch*K + e] = sum over stages s of
+ * code_s << (3 s), code_s = 0 (not troubled, SlopeLimitN.m:23) or 4 | (active minmod
+ * argument 0..3, minmod.m:9-11).  dg_lserk4_adj_ex reads the record back. */
+int dg_lserk4_fwd_ex(dg_plan* plan, double* u, double t0, double dt, int nsteps,
+                     double* snapshots, uint16_t* decisions, void* stream);
+
 /* Adjoint sweep + dual-weighted residual (the "adj_march" / "adjoint_sens" / "err_contribution"
  * role; discrete-adjoint pattern python/Main_finite_difference.py:54-76, indicator pattern :79-94).
  * Exact discrete transpose of the forward step, run for n = nsteps-1 .. 0:
@@ -162,10 +170,15 @@ int dg_lserk4_adj(dg_plan* plan, double* w, const double* snapshots, double t0, 
  *                      caller need not zero it (nsteps = 0: eta is zeroed)
  *   DG_ADJ_ETA_ABS     the sweep's last launch stores |eta|: the per-trajectory magnitude the
  *                      reference's errorIndicator returns (python/Main_width_ref.py:139,
- *                      `return jnp.abs(err)`) before its mean over ICs (:479) */
+ *                      `return jnp.abs(err)`) before its mean over ICs (:479)
+ * decisions (nullable, plans with a per-stage limiter only; ignored otherwise): the record
+ * dg_lserk4_fwd_ex wrote for the same sweep.  The adjoint then takes the limiter's frozen
+ * decisions from it instead of re-testing every cell, and skips the limiter work and its
+ * exchange in every stage where no cell of a tile is troubled (bit-identical results). */
 enum { DG_ADJ_ETA_ASSIGN = 1, DG_ADJ_ETA_ABS = 2 };
 int dg_lserk4_adj_ex(dg_plan* plan, double* w, const double* snapshots, double t0, double dt,
-                     int nsteps, double src_coef, double* eta, int flags, void* stream);
+                     int nsteps, double src_coef, double* eta, int flags,
+                     const uint16_t* decisions, void* stream);
 
 /* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */

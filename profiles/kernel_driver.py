@@ -1,13 +1,18 @@
 """Minimal driver for counter collection on one step kernel (no timing, no checks):
 
   python profiles/kernel_driver.py --what fwd_nosnap|fwd|adj [--N 4] [--K 1048576] [--reps 3]
+                                   [--physics linear|burgers_limited] [--nonuniform]
 
-Runs `reps` sweeps of 20 steps of the chosen kernel after one warm-up sweep."""
+Runs `reps` sweeps of --nsteps steps of the chosen kernel after one warm-up sweep.
+--physics burgers_limited is BASELINE config 3 (Burgers flux + SlopeLimitN per stage);
+--nonuniform splits one element first, as the config-3 refine loop does, so the kernels run
+their non-uniform-mesh specialisation."""
 import argparse
 import importlib
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,11 +26,22 @@ def main():
   p.add_argument("--K", type=int, default=1 << 20)
   p.add_argument("--nsteps", type=int, default=20)
   p.add_argument("--reps", type=int, default=3)
-  p.add_argument("--steps-per-launch", type=int, default=4)
+  p.add_argument("--steps-per-launch", type=int, default=None)
+  p.add_argument("--physics", default="linear", choices=("linear", "burgers_limited"))
+  p.add_argument("--nonuniform", action="store_true")
   a = p.parse_args()
   pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
-  mesh = pkg.BaseGalerkin1D(n=a.N, k=a.K)
-  op = pkg.operators.DGAdvection1D(mesh).tune(steps_per_launch=a.steps_per_launch)
+  v_x = np.linspace(0.0, 1.0, a.K + 1)
+  if a.nonuniform:
+    v_x = np.insert(v_x, a.K // 3 + 1, 0.5 * (v_x[a.K // 3] + v_x[a.K // 3 + 1]))[:-1]
+    v_x = v_x / v_x[-1]
+  mesh = pkg.BaseGalerkin1D(n=a.N, v_x=v_x)
+  kw = {} if a.physics == "linear" else dict(flux="burgers", limiter=True)
+  op = pkg.operators.DGAdvection1D(mesh, **kw)
+  if a.steps_per_launch is not None:
+    op.tune(steps_per_launch=a.steps_per_launch)
+  elif a.physics == "linear":
+    op.tune(steps_per_launch=4)
   dt = mesh.cfl_dt()
   snaps = op.new_field(a.nsteps + 1)
   op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
@@ -43,7 +59,7 @@ def main():
       w.copy_(snaps[a.nsteps])
       op.adjoint(w, snaps, 0.0, dt, a.nsteps, eta=eta)
   torch.cuda.synchronize()
-  print("ok", a.what)
+  print("ok", a.what, a.physics, "uniform" if op.uniform else "nonuniform")
 
 
 if __name__ == "__main__":

@@ -350,7 +350,8 @@ def test_kernel_variants_bit_identical(pkg, gpu, N, K):
   outs = []
   nsteps = 7  # exercises the greedy 4 + 2 + 1 chunking
   shapes = ((1, 1, 1, 0), (2, 1, 0, 0), (1, 2, 1, 0), (1, 4, 1, 0), (2, 4, 0, 0), (1, 4, 0, 0),
-            (2, 2, 1, 0), (1, 4, 1, 4), (1, 4, 1, 2), (1, 2, 1, 4), (2, 8, 1, 0))
+            (2, 2, 1, 0), (1, 4, 1, 4), (1, 4, 1, 2), (1, 2, 1, 4), (2, 8, 1, 0), (2, 8, 1, 4),
+            (2, 8, 1, 8), (2, 8, 1, 2))
   for width, ms, xcd, lanes in shapes:
     if lanes and N == 8:
       lanes = 0  # wave tiles cover Np <= 8
@@ -370,7 +371,9 @@ def test_kernel_variants_bit_identical(pkg, gpu, N, K):
   for a_, b_ in zip(outs[0], outs[1]):
     np.testing.assert_array_equal(a_, b_)
   # same steps per launch, other lane packing / tile order / wave tiles
-  for i, j in ((3, 4), (3, 5), (3, 7), (3, 8), (2, 9)):
+  # (8-step launches on wave tiles: 4 and 8 elements per lane; with 2 elements per lane the
+  # plan caps the launch at 4 steps, so shape 13 equals shape 3's 4-step sweep)
+  for i, j in ((3, 4), (3, 5), (3, 7), (3, 8), (2, 9), (10, 11), (10, 12), (3, 13)):
     for a_, b_ in zip(outs[i], outs[j]):
       np.testing.assert_array_equal(a_, b_)
   # States agree to 1e-12; the indicator (a cancellation-limited jump residual) to RTOL.
