@@ -177,6 +177,24 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
         }
       }
     }
+#ifdef DG_DIRECT_STORE  // experiment: each lane stores its element from registers, no LDS pass
+    if (!EDGE && (snap != nullptr || st == MS - 1)) {
+      if (E[0].valid) {
+        double u[NP];
+        from_eo<NP>(ev[0], od[0], u);
+        if (snap != nullptr) {
+          double* o = snap + st * args.stride + E[0].e * NP;
+#pragma unroll
+          for (int i = 0; i < NP; ++i) o[i] = u[i];
+        }
+        if (st == MS - 1 && last != nullptr) {
+#pragma unroll
+          for (int i = 0; i < NP; ++i) last[E[0].e * NP + i] = u[i];
+        }
+      }
+      continue;
+    }
+#endif
     if (snap != nullptr || st == MS - 1) {
       // The image's last readers (staging reads, the previous step's store) are at least
       // one stage barrier behind; the faces live elsewhere.
@@ -202,6 +220,9 @@ __global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* 
   using G = TileGeo<NP, W>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * NS];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+#ifdef DG_SETPRIO_ODD  // experiment: desynchronise co-resident workgroups (MI355X_MICROARCH.md)
+  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
   if (edge_tile(e0, G::T, args.ktot, args.K))
     step_tile<NP, NS, UNI, W, MS, true>(lds, tile, uin, snap, last, scale, args);
@@ -423,6 +444,9 @@ __global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(co
   using G = TileGeo<NP, W>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS + 1];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+#ifdef DG_SETPRIO_ODD  // experiment: desynchronise co-resident workgroups (MI355X_MICROARCH.md)
+  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
   if (edge_tile(e0, G::T, args.ktot, args.K))
     adj_tile<NP, NS, UNI, W, MS, true>(lds, tile, win, wout, snap, eta, scale, args);
@@ -961,12 +985,12 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
 
   // Per-N default shape (config 5 sweeps, profiles/r01/tune/N*.json and
   // profiles/r02/tune/): 512-element tiles pay off at low order, where a lane's work per
-  // stage is small; at N = 1 the forward runs on one-wave tiles of 4 elements per lane
-  // (DPP face exchange, no barriers: 23.8 -> 18.9 us per 4-step launch), at N = 2 both
-  // directions take 8 steps per launch (bench 3.82e11 -> 4.03e11 DOF-updates/s).
+  // stage is small; at N = 1 and 2 the forward runs on one-wave tiles of 4 elements per lane
+  // (DPP face exchange, no workgroup barriers): 23.8 -> 18.9 us (N = 1) and 27.7 -> 24.8 us
+  // (N = 2) per 4-step launch.  (8 steps per launch at N = 2 bench the same within noise but
+  // leave a 4-step launch in a 20-step sweep.)
   p->tile_width = (N <= 2) ? 2 : 1;
-  if (N == 1) p->lane_elems = 4;
-  if (N == 2) p->msteps = 8;
+  if (N <= 2) p->lane_elems = 4;
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);

@@ -389,6 +389,12 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
+  // The decision record is loaded first, with the tiles, so its latency hides behind theirs.
+  int kcode = 0;
+  if constexpr (KNOWN) {
+    const int64_t e = e0 + lane;
+    kcode = (e >= 0 && e < args.ktot) ? int(codes[e]) : 0;
+  }
   TileRegs<NP, W> pu, pw;
   tile_issue<NP, W, EDGE>(snap, e0, nd, pu);
   tile_issue<NP, W, EDGE>(win, e0, nd, pw);
@@ -426,11 +432,10 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   //    KNOWN: the decisions are the forward sweep's record; `wg` (the OR over the tile's
   //    lanes) says in which stages some cell of the tile is troubled at all -- in the
   //    others the limiter and its exchange are skipped, here and in the reverse pass.
-  int kcode = 0, wg = 0;
+  int wg = 0;
   if constexpr (KNOWN) {
     // bitwise OR of the tile's records (__syncthreads_or would only say "some nonzero")
     __shared__ int wg_or;
-    kcode = E.inrange ? int(codes[E.e]) : 0;
     if (lane == 0) wg_or = 0;
     __syncthreads();
     if (kcode != 0) atomicOr(&wg_or, kcode);  // LDS atomic, rare lanes only
@@ -499,6 +504,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 
   // 4. Reverse stages s = 4..0 (forward: r = A_s r + dt L f(u); v = u + B_s r; u = Lim(v)):
   //      lv = Lim'(v)^T lu;  lr += B_s lv;  lu = lv + f'(u_s) (dt L^T lr);  lr = A_s lr.
+  double un[NP];  // u_0 = u^n for the last reverse stage, re-read from the snapshot early
   double lre[NE], lro[NO];
 #pragma unroll
   for (int k = 0; k < NE; ++k) lre[k] = 0.0;
@@ -507,6 +513,10 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 #pragma unroll
   for (int ss = 0; ss < 5; ++ss) {
     const int s = 4 - ss;
+    if (BURG && s == 2) {  // issue the re-read two stages ahead (u_4, u_3 are dead by now)
+#pragma unroll
+      for (int i = 0; i < NP; ++i) un[i] = E.inrange ? snap[E.e * NP + i] : 0.0;
+    }
     if (LIM && (!KNOWN || ((wg >> (3 * s)) & 4))) {  // (workgroup-uniform)
       // Transposed limiter.  Troubled cell: y = v_avg + (r/2) hm, hm one of
       // {2 (Dr V)(1,:) uh(1:2), v+ - v, v - v-} (or 0): the cell's own nodal adjoint is
@@ -613,9 +623,6 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 #pragma unroll
         for (int k = 0; k < NO; ++k) uo[k] = lds[SE1 + (NE + k) * T + lane];
       } else {
-        double un[NP];
-#pragma unroll
-        for (int i = 0; i < NP; ++i) un[i] = E.inrange ? snap[E.e * NP + i] : 0.0;
         to_eo<NP>(un, ue, uo);
       }
 #pragma unroll

@@ -402,16 +402,21 @@ def main_config3(args, world, rank, dev):
     dist.destroy_process_group()
 
 
-def launches_per_sweep(nsteps, ms):
-  """The library's greedy chunking of a sweep into launches of <= ms steps."""
-  launches, left = 0, nsteps
+def sweep_chunks(nsteps, ms):
+  """The library's greedy chunking of a sweep into launches of <= ms steps (dg_advec.hip
+  chunk()): the steps of each launch."""
+  chunks, left = [], nsteps
   while left > 0:
     m = ms
     while m > left:
       m //= 2
     left -= m
-    launches += 1
-  return launches
+    chunks.append(m)
+  return chunks
+
+
+def launches_per_sweep(nsteps, ms):
+  return len(sweep_chunks(nsteps, ms))
 
 
 def main(argv=None):
@@ -495,18 +500,21 @@ def main(argv=None):
 
   Np, ktot = N + 1, K * sweep.batch
   ms = sweep.op.steps_per_launch
-  launches = launches_per_sweep(nsteps, ms)
+  chunks = sweep_chunks(nsteps, ms)
+  launches = len(chunks)
   fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / launches for e in evs]
   adj_us = [e[1].elapsed_time(e[2]) * 1e3 / launches for e in evs]
   step_ms = [evs[i][0].elapsed_time(evs[i + 1][0] if i + 1 < len(evs) else ev_end)
              for i in range(len(evs))]
   fwd_launch_us, adj_launch_us = float(np.mean(fwd_us)), float(np.mean(adj_us))
-  # Algorithmic bytes per launch of `ms` fused steps:
-  #   forward: read u^n once, write the ms snapshots u^{n+1..n+ms}:  (8 + 8 ms) B per DOF
-  #   adjoint: read w^{n+ms}, read the ms snapshots, write w^n: (16 + 8 ms) B per DOF,
+  # Algorithmic bytes of a launch of m fused steps:
+  #   forward: read u^n once, write the m snapshots u^{n+1..n+m}:  (8 + 8 m) B per DOF
+  #   adjoint: read w^{n+m}, read the m snapshots, write w^n: (16 + 8 m) B per DOF,
   #            plus the indicator read-modify-write, 16 B per element.
-  fwd_bytes = (8.0 + 8.0 * ms) * Np * ktot
-  adj_bytes = (16.0 + 8.0 * ms) * Np * ktot + 16.0 * ktot
+  # A sweep's launches may differ in m (e.g. 8 + 8 + 4 at 20 steps); the per-launch figures
+  # are the sweep's averages: achieved = sweep bytes / sweep time.
+  fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in chunks]))
+  adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
@@ -579,6 +587,7 @@ def main(argv=None):
                       "adj_frac_of_achievable": adj_gbs / copy_gbs if copy_gbs else None,
                       "fwd_frac_of_achievable": fwd_gbs / copy_gbs if copy_gbs else None},
       "steps_per_launch": ms,
+      "launch_steps": chunks,
       "refine_index": ref_idx,
       "refine_value": ref_val,
       "refine_index_ranks": idx_ranks,

@@ -45,7 +45,10 @@ def main():
   dt = mesh.cfl_dt()
   snaps = op.new_field(a.nsteps + 1)
   op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
-  op.forward(snaps[0], 0.0, dt, a.nsteps, snaps)
+  # limited plans: the forward's decision record, read back by the adjoint (as AdaptiveSweep)
+  rec = (torch.zeros(a.nsteps * op.ktot, dtype=torch.int16, device=op.device)
+         if op.limiter else None)
+  op.forward(snaps[0], 0.0, dt, a.nsteps, snaps, decisions=rec)
   w = op.new_field()
   eta = torch.zeros(op.ktot, dtype=torch.float64, device=op.device)
   u = op.new_field()
@@ -54,10 +57,10 @@ def main():
       u.copy_(snaps[0])
       op.forward(u, 0.0, dt, a.nsteps)
     elif a.what == "fwd":
-      op.forward(snaps[0], 0.0, dt, a.nsteps, snaps)
+      op.forward(snaps[0], 0.0, dt, a.nsteps, snaps, decisions=rec)
     else:
       w.copy_(snaps[a.nsteps])
-      op.adjoint(w, snaps, 0.0, dt, a.nsteps, eta=eta)
+      op.adjoint(w, snaps, 0.0, dt, a.nsteps, eta=eta, decisions=rec)
   torch.cuda.synchronize()
   print("ok", a.what, a.physics, "uniform" if op.uniform else "nonuniform")
 
