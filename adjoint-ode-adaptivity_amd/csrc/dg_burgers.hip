@@ -88,11 +88,13 @@ __device__ __forceinline__ void flux_eo(const double* ev, const double* od, doub
 
 // Exchange arrays in LDS (doubles, each padded by one slot on the left): two
 // double-buffered face pairs [0, 4(T+2)), cell averages [4(T+2), 5(T+2)), the adjoint's
-// limiter contributions to the left / right neighbour [5(T+2), 7(T+2)).
+// limiter contributions to the left / right neighbour [5(T+2), 7(T+2)), the indicator's
+// face values of u^{n+1} [7(T+2), 9(T+2)) (exchanged with the first reverse stage's).
 template <int NP, int W = 1> struct NLGeo {
   static constexpr int T = kBlock * W;
   static constexpr int FA = 4 * (T + 2), CL = 5 * (T + 2), CR = 6 * (T + 2);
-  static constexpr int kEx = 7 * (T + 2);
+  static constexpr int IL = 7 * (T + 2), IR = 8 * (T + 2);
+  static constexpr int kEx = 9 * (T + 2);
   static constexpr int kTileD = T * NP + 2;
   static constexpr int kLds = kTileD > kEx ? kTileD : kEx;  // boundary constants follow
 };
@@ -480,27 +482,21 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     }
     if constexpr (NE > NO) we[NO] = fma(args.src, ev[NO], we[NO]);
   }
-  // 3. Indicator: eta += dt sum_i w_i (LIFT Fscale du)_i at u^{n+1}, t_{n+1}.
-  double eacc = 0.0;
+  // 3. Indicator: eta += dt sum_i w_i (LIFT Fscale du)_i at u^{n+1}, t_{n+1}.  The weights
+  //    (le.we, lo.wo) are local; the neighbours' face fluxes of u^{n+1} travel with the
+  //    first reverse stage's exchange below (one barrier fewer per step).
+  double eacc = 0.0, ipe = 0.0, ipo = 0.0, uf0 = 0.0, ufN = 0.0;
   if (args.has_eta) {
     double fe[NE], fo[NO];
     flux_eo<NP, BURG>(ev, od, fe, fo);
-    const double f0 = fe[0] + fo[0], fN = fe[0] - fo[0];
-    constexpr int gL = 2 * (T + 2), gR = gL + (T + 2);  // face buffer 1 (stage 4 used 0)
-    lds[gL + lane + 1] = f0;
-    lds[gR + lane + 1] = fN;
-    __syncthreads();
-    const double du0 = f0 - lds[EDGE && E.first ? CB + 5 : gR + lane];
-    const double du1 = fN - lds[EDGE && E.last ? gR + lane + 1 : gL + lane + 2];
-    double pe = 0.0, po = 0.0;
+    uf0 = fe[0] + fo[0];
+    ufN = fe[0] - fo[0];
 #pragma unroll
-    for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[k], pe);
+    for (int k = 0; k < NE; ++k) ipe = fma(args.op.le[k], we[k], ipe);
 #pragma unroll
-    for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[k], po);
-    eacc = fma(du0 - du1, pe, (du0 + du1) * po);
-    if constexpr (!UNI) eacc *= sc;
+    for (int k = 0; k < NO; ++k) ipo = fma(args.op.lo[k], wo[k], ipo);
   }
-  __syncthreads();  // exchange reads of the last stage / the indicator are done
+  constexpr int IL = NLGeo<NP, W>::IL, IR = NLGeo<NP, W>::IR;
 
   // 4. Reverse stages s = 4..0 (forward: r = A_s r + dt L f(u); v = u + B_s r; u = Lim(v)):
   //      lv = Lim'(v)^T lu;  lr += B_s lv;  lu = lv + f'(u_s) (dt L^T lr);  lr = A_s lr.
@@ -559,7 +555,9 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 #pragma unroll
       for (int k = 0; k < NE; ++k) we[k] = fma(alpha, args.lc.a0e[k], we[k]);
     }
-    const int f0 = (ss & 1) * 2 * (T + 2), f1 = f0 + (T + 2);
+    // Face buffers alternate starting with buffer 1: the recompute's last stage read
+    // buffer 0 after its barrier, and no barrier separates it from this first write.
+    const int f0 = ((ss + 1) & 1) * 2 * (T + 2), f1 = f0 + (T + 2);
     double qe[NE], qo[NO];
     double gd = 0.0, gs = 0.0;
     // transpose of v = u + (B_s sc) r' (nl_stage's metric folding): lr' += (B_s sc) lv
@@ -581,6 +579,10 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     if constexpr (EDGE) g1 = E.last ? 0.0 : g1;
     lds[f0 + lane + 1] = g0;
     lds[f1 + lane + 1] = g1;
+    if (ss == 0 && args.has_eta) {  // the indicator's u^{n+1} faces ride along
+      lds[IL + lane + 1] = uf0;
+      lds[IR + lane + 1] = ufN;
+    }
     __builtin_amdgcn_sched_barrier(0);
     double pe[NE], po[NO];  // transposed volume term: the adjoint of the flux values
 #pragma unroll
@@ -606,6 +608,15 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 #pragma unroll
     for (int k = 0; k < NO; ++k) pin(po[k]);
     __syncthreads();
+    if (ss == 0 && args.has_eta) {
+      // left neighbour's right face / right neighbour's left face of u^{n+1}; a
+      // trajectory's first element reads the inflow flux at t_{n+1}, its last one its own
+      // right face (du1 = 0)
+      const double du0 = uf0 - lds[EDGE && E.first ? CB + 5 : IR + lane];
+      const double du1 = ufN - lds[EDGE && E.last ? IR + lane + 1 : IL + lane + 2];
+      eacc = fma(du0 - du1, ipe, (du0 + du1) * ipo);
+      if constexpr (!UNI) eacc *= sc;
+    }
     const double gl = lds[EDGE && E.first ? CB + 6 : f1 + lane];
     const double gr = lds[EDGE && E.last ? CB + 6 : f0 + lane + 2];
     pe[0] += (g0 + g1) - (gr + gl);
