@@ -60,15 +60,21 @@ __device__ __forceinline__ double minmod_br(double a, double b, double c, int& b
 }
 
 // The troubled-cell test of SlopeLimitN.m:21-23.  Both minmods share the neighbour
-// differences b = v - v-, c = v+ - v; with all three arguments of one sign minmod is their
-// min (all > 0) or max (all < 0), exactly as s*min|.| (minmod.m:9-11), else 0.
+// differences b = v - v-, c = v+ - v; with all three arguments of one sign minmod is the
+// argument of least magnitude (minmod.m:9-11: s*min|.|), else 0.  Written as selects on
+// magnitude compares (abs is a free operand modifier): no fmin/fmax, whose IEEE-mode
+// operand canonicalisation costs two extra VALU ops each, and no branches.  On ties the two
+// candidates are equal, so the pick is the same value s*min|.| gives; a NaN fails every
+// sign test and yields 0, as in minmod.
 __device__ __forceinline__ bool troubled(double v, double vm, double vp, double u0, double uN) {
   const double b = v - vm, c = vp - v;
   const bool bcp = b > 0.0 && c > 0.0, bcn = b < 0.0 && c < 0.0;
-  const double mn = fmin(b, c), mx = fmax(b, c);
+  const double bc = fabs(b) < fabs(c) ? b : c;
   const double a1 = v - u0, a2 = uN - v;
-  const double m1 = (bcp && a1 > 0.0) ? fmin(a1, mn) : ((bcn && a1 < 0.0) ? fmax(a1, mx) : 0.0);
-  const double m2 = (bcp && a2 > 0.0) ? fmin(a2, mn) : ((bcn && a2 < 0.0) ? fmax(a2, mx) : 0.0);
+  const double s1 = fabs(a1) < fabs(bc) ? a1 : bc;
+  const double s2 = fabs(a2) < fabs(bc) ? a2 : bc;
+  const double m1 = ((bcp && a1 > 0.0) || (bcn && a1 < 0.0)) ? s1 : 0.0;
+  const double m2 = ((bcp && a2 > 0.0) || (bcn && a2 < 0.0)) ? s2 : 0.0;
   return fabs((v - m1) - u0) > 1.0e-8 || fabs((v + m2) - uN) > 1.0e-8;
 }
 
@@ -116,8 +122,9 @@ template <int NP, int W = 1> struct NLGeo {
 template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE, bool KNOWN, int W>
 __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s, int par, int iin,
                                         const Elem& E, double sc, const EOArgs<NP>& op,
-                                        const LimEO<NP>& lc, double* ev, double* od,
-                                        double* re, double* ro, int kc = 0, bool any = true) {
+                                        const LimEO<NP>& lc, const LimEO<NP>& lk, double* ev,
+                                        double* od, double* re, double* ro, int kc = 0,
+                                        bool any = true) {
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, T = kBlock * W;
   constexpr int FA = NLGeo<NP, W>::FA;
   // par: face buffer, alternating over consecutive stages (across steps too: without the
@@ -195,16 +202,17 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
       const double a1 = fma(lc.dv0, avg, lc.dv1 * uh1);
       hm = br == 1 ? a1 : (br == 2 ? ap - avg : (br == 3 ? avg - am : 0.0));
     } else {
-      if (!lc.every && !troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0])) return 0;
-      uh1 = lc.a1o[0] * od[0];
+      // (the test runs unconditionally: a branch on `every` only splits the code)
+      if (!(troubled(avg, am, ap, ev[0] + od[0], ev[0] - od[0]) | (lc.every != 0))) return 0;
+      uh1 = lk.a1o[0] * od[0];
 #pragma unroll
-      for (int k = 1; k < NO; ++k) uh1 = fma(lc.a1o[k], od[k], uh1);
-      hm = minmod_br(fma(lc.dv0, avg, lc.dv1 * uh1), ap - avg, avg - am, br);
+      for (int k = 1; k < NO; ++k) uh1 = fma(lk.a1o[k], od[k], uh1);
+      hm = minmod_br(fma(lk.dv0, avg, lk.dv1 * uh1), ap - avg, avg - am, br);
     }
 #pragma unroll
     for (int k = 0; k < NE; ++k) ev[k] = avg;
 #pragma unroll
-    for (int k = 0; k < NO; ++k) od[k] = lc.rco[k] * hm;
+    for (int k = 0; k < NO; ++k) od[k] = lk.rco[k] * hm;
     return 4 | br;
   }
 }
@@ -301,6 +309,12 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
   if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
   __syncthreads();  // the exchange arrays alias the staging image
 
+  // The troubled-cell branch's constants are read from the kernel-argument segment where
+  // they are used (scalar loads inside the rare branch) rather than kept live in SGPRs for
+  // the whole tile: under the 80-SGPR cap that keeps every other constant unspilled.
+  using SArgs = NLStepArgs<NP, MS>;
+  const LimEO<NP>& lk = *reinterpret_cast<const LimEO<NP>*>(
+      kernarg_tail<decltype(&k_step_nl<NP, BURG, LIM, UNI, MS>), SArgs>() + offsetof(SArgs, lc));
   double re[NE], ro[NO];
 #pragma unroll
   for (int st = 0; st < MS; ++st) {
@@ -309,7 +323,7 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
     for (int s = 0; s < 5; ++s)
       c15 |= nl_stage<NP, BURG, LIM, UNI, EDGE, false, W>(lds, lane, s, (st * 5 + s) & 1,
                                                           CB + st * 5 + s, E, sc, args.op, args.lc,
-                                                          ev, od, re, ro)
+                                                          lk, ev, od, re, ro)
              << (3 * s);
     // The decision record for the adjoint (dg_lserk4_fwd_ex): one 16-bit word per element
     // and step, written by the lane that owns the element.
@@ -467,7 +481,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
         for (int k = 0; k < NO; ++k) lds[SE1 + (NE + k) * T + lane] = od[k];
       }
       const int c = nl_stage<NP, BURG, LIM, UNI, EDGE, KNOWN, W>(
-          lds, lane, s, s & 1, CB + s, E, sc, args.op, args.lc, ev, od, re, ro,
+          lds, lane, s, s & 1, CB + s, E, sc, args.op, args.lc, args.lc, ev, od, re, ro,
           (kcode >> (3 * s)) & 7, ((wg >> (3 * s)) & 4) != 0);
       if constexpr (LIM) dcodes |= c << (3 * s);
     }
