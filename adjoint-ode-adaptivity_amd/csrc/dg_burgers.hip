@@ -289,6 +289,9 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
   const int64_t rem = nd - o0;
   const int64_t count = rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP;
 
+  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  double sc = args.sc;
+  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;  // issued with the tile's loads
   TileRegs<NP, W> pf;
   tile_issue<NP, W, EDGE>(uin, e0, nd, pf);
   tile_commit<NP, W>(pf, lds);
@@ -304,9 +307,6 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
   __syncthreads();
   double ev[NE], od[NO];
   to_eo<NP>(lds + pf.off + lane * NP, ev, od);
-  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
-  double sc = args.sc;
-  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
   __syncthreads();  // the exchange arrays alias the staging image
 
   // The troubled-cell branch's constants are read from the kernel-argument segment where
@@ -411,10 +411,18 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     const int64_t e = e0 + lane;
     kcode = (e >= 0 && e < args.ktot) ? int(codes[e]) : 0;
   }
+  // the element's metric likewise
+  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  double sc = args.sc;
+  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
   TileRegs<NP, W> pu, pw;
   tile_issue<NP, W, EDGE>(snap, e0, nd, pu);
   tile_issue<NP, W, EDGE>(win, e0, nd, pw);
   tile_commit<NP, W>(pu, lds);
+  // KNOWN: bitwise OR of the tile's records (__syncthreads_or would only say "some
+  // nonzero"), cleared here and OR-ed between the load phase's barriers
+  __shared__ int wg_or;
+  if (KNOWN && lane == 0) wg_or = 0;
   if constexpr (EDGE) {
     using AArgs = NLAdjArgs<NP>;  // the args follow the pointer arguments of k_adj_nl
     const double* ka = reinterpret_cast<const double*>(
@@ -426,6 +434,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   __syncthreads();
   double ev[NE], od[NO];
   to_eo<NP>(lds + pu.off + lane * NP, ev, od);
+  if (KNOWN && kcode != 0) atomicOr(&wg_or, kcode);  // LDS atomic, rare lanes only
   __syncthreads();
   tile_commit<NP, W>(pw, lds);
   __syncthreads();
@@ -439,9 +448,6 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     }
     if constexpr (NE > NO) we[NO] = w[NO];
   }
-  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
-  double sc = args.sc;
-  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
   __syncthreads();  // the exchange arrays alias the staging image
 
   // 1. Recompute the step's stages, keeping each stage's input and limiter decision.
@@ -449,15 +455,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   //    lanes) says in which stages some cell of the tile is troubled at all -- in the
   //    others the limiter and its exchange are skipped, here and in the reverse pass.
   int wg = 0;
-  if constexpr (KNOWN) {
-    // bitwise OR of the tile's records (__syncthreads_or would only say "some nonzero")
-    __shared__ int wg_or;
-    if (lane == 0) wg_or = 0;
-    __syncthreads();
-    if (kcode != 0) atomicOr(&wg_or, kcode);  // LDS atomic, rare lanes only
-    __syncthreads();
-    wg = wg_or;
-  }
+  if constexpr (KNOWN) wg = wg_or;  // the load phase's barriers ordered its init and ORs
   // The stage inputs u_s feed the Burgers flux Jacobian of the reverse pass.  Registers
   // hold u_2..u_4; u_1 goes to a lane-private LDS slot and u_0 = u^n is re-read from the
   // snapshot (L2-resident) at the end: 20 VGPRs fewer at the peak (5 waves per SIMD
