@@ -80,16 +80,22 @@ __device__ __forceinline__ bool troubled(double v, double vm, double vp, double 
 
 // Flux values divided by a, in even/odd coordinates: f = u (linear) or u^2/2 (Burgers):
 //   fe_k = (f_k + f_{N-k})/2 = (e^2 + o^2)/2,  fo_k = (f_k - f_{N-k})/2 = e o.
-template <int NP, bool BURG>
+// HQ (Burgers only): fe is returned doubled, for a Qoe the host pre-halved -- halving is
+// exact, so (Qoe/2) (2 fe) rounds exactly as Qoe fe, and a face value fe_0 + fo_0 becomes
+// fma(0.5, 2 fe_0, fo_0), the same number: NE multiplies fewer per stage, bit-identical.
+template <int NP, bool BURG, bool HQ = false>
 __device__ __forceinline__ void flux_eo(const double* ev, const double* od, double* fe,
                                         double* fo) {
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
+  static_assert(BURG || !HQ, "HQ is the Burgers flux's option");
 #pragma unroll
   for (int k = 0; k < NO; ++k) {
-    fe[k] = BURG ? 0.5 * fma(ev[k], ev[k], od[k] * od[k]) : ev[k];
+    fe[k] = BURG ? (HQ ? fma(ev[k], ev[k], od[k] * od[k])
+                       : 0.5 * fma(ev[k], ev[k], od[k] * od[k]))
+                 : ev[k];
     fo[k] = BURG ? ev[k] * od[k] : od[k];
   }
-  if constexpr (NE > NO) fe[NO] = BURG ? 0.5 * ev[NO] * ev[NO] : ev[NO];
+  if constexpr (NE > NO) fe[NO] = BURG ? (HQ ? ev[NO] * ev[NO] : 0.5 * ev[NO] * ev[NO]) : ev[NO];
 }
 
 // Exchange arrays in LDS (doubles, each padded by one slot on the left): two
@@ -119,7 +125,7 @@ template <int NP, int W = 1> struct NLGeo {
 // instead of the troubled-cell test, and `any` (workgroup-uniform: some lane of the tile is
 // troubled in this stage) gates the cell-average exchange: a stage without a troubled cell
 // in the tile runs no limiter work and no second barrier.
-template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE, bool KNOWN, int W>
+template <int NP, bool BURG, bool LIM, bool UNI, bool EDGE, bool KNOWN, int W, bool HQ = false>
 __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s, int par, int iin,
                                         const Elem& E, double sc, const EOArgs<NP>& op,
                                         const LimEO<NP>& lc, const LimEO<NP>& lk, double* ev,
@@ -131,8 +137,9 @@ __device__ __forceinline__ int nl_stage(double* __restrict__ lds, int el, int s,
   // limiter no barrier separates a step's last face reads from the next step's writes)
   const int fL = par * 2 * (T + 2), fR = fL + (T + 2);
   double fe[NE], fo[NO];
-  flux_eo<NP, BURG>(ev, od, fe, fo);
-  const double f0 = fe[0] + fo[0], fN = fe[0] - fo[0];
+  flux_eo<NP, BURG, HQ>(ev, od, fe, fo);
+  const double f0 = HQ ? fma(0.5, fe[0], fo[0]) : fe[0] + fo[0];
+  const double fN = HQ ? fma(0.5, fe[0], -fo[0]) : fe[0] - fo[0];
   lds[fL + el + 1] = f0;
   lds[fR + el + 1] = fN;
   __builtin_amdgcn_sched_barrier(0);
@@ -321,7 +328,7 @@ __device__ __forceinline__ void nl_step_tile(double* __restrict__ lds, int64_t t
     int c15 = 0;  // this step's limiter decisions, 3 bits per stage
 #pragma unroll
     for (int s = 0; s < 5; ++s)
-      c15 |= nl_stage<NP, BURG, LIM, UNI, EDGE, false, W>(lds, lane, s, (st * 5 + s) & 1,
+      c15 |= nl_stage<NP, BURG, LIM, UNI, EDGE, false, W, BURG>(lds, lane, s, (st * 5 + s) & 1,
                                                           CB + st * 5 + s, E, sc, args.op, args.lc,
                                                           lk, ev, od, re, ro)
              << (3 * s);
@@ -785,6 +792,8 @@ int launch_step_nl(const dg_plan* p, const double* in, double* snap, double* las
   // constants carry dt (and 2/h on uniform meshes); non-uniform meshes multiply the update
   // by the element's 2/h (nl_stage's metric folding)
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : dt, &a.op);
+  if (BURG)  // the forward's nl_stage takes the Burgers fe doubled (flux_eo HQ)
+    for (double& q : a.op.Qoe) q *= 0.5;
   a.lc = make_lim_eo<NP>(p);
   a.sc = 1.0;
   for (int m = 0; m < MS; ++m)
