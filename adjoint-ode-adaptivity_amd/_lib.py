@@ -49,6 +49,10 @@ SIGNATURES = {
                                 ctypes.c_double, _vp, _i32, _vp, _vp]),
     "dg_lserk4_fwd_ex": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp,
                                 _vp]),
+    "dg_lserk4_fwd_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,
+                                 _vp]),
+    "dg_lserk4_adj_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,
+                                 _i32, _vp]),
     "dg_slope_limit_n": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dg_slope_limit_1": (_i32, [_vp, _vp, _vp, _vp]),
     "dg_argmax": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),

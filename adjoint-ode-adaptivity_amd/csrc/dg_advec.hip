@@ -31,13 +31,13 @@ int fail(int code, const std::string& msg) {
 namespace {
 using namespace dgk;
 
-template <int NP, int NS, bool UNI, int W, int MS>
+template <int NP, int NS, bool UNI, int W, int MS, bool REC>
 __global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* __restrict__ uin,
                                                      double* __restrict__ snap,
                                                      double* __restrict__ last,
                                                      const double* __restrict__ scale,
                                                      StepArgs<NP, NS, MS> args);
-template <int NP, int NS, bool UNI, int W, int MS>
+template <int NP, int NS, bool UNI, int W, int MS, bool REC>
 __global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(const double* __restrict__ win,
                                                     double* __restrict__ wout,
                                                     const double* __restrict__ snap,
@@ -45,13 +45,23 @@ __global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(co
                                                     const double* __restrict__ scale,
                                                     AdjArgs<NP, MS> args);
 
+// The jump record (dg_lserk4_fwd_rec / dg_lserk4_adj_rec).  The indicator needs of u^n only
+// the two interelement jumps of each element, du0 = u_0 - uL and du1 = u_N - uR (the DWR
+// residual R(u^n) = LIFT Fscale du, utils/AdvecRHS1D.m:19): the forward records, per element
+// and step, (du0 - du1, du0 + du1) -- 16 bytes where a snapshot takes 8 Np -- computed from
+// the face values its stage 0 exchanges anyway, with exactly the adjoint's arithmetic, so
+// eta is bit-identical to the snapshot sweep's.  Record n-1 holds u^n's jumps, n = 1..nsteps.
+__device__ __forceinline__ double2* jump_slot(double* rec, int64_t n, int64_t ktot, int64_t e) {
+  return reinterpret_cast<double2*>(rec) + (n * ktot + e);
+}
+
 // ---------------------------------------------------------------------------
 // Forward fused kernel: MS time steps of NS stages (AdvecRHS1D + the low-storage update)
 // for the EPL elements of each lane.  After each step st the interior elements go to
 // snap + st*stride (if snap) and after the last step also to `last` (if non-null).
 // UNI: the operator constants already carry dt*2/h.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int W, int MS, bool EDGE>
+template <int NP, int NS, bool UNI, int W, int MS, bool REC, bool EDGE>
 __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile,
                                           const double* __restrict__ uin,
                                           double* __restrict__ snap, double* __restrict__ last,
@@ -59,7 +69,9 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
                                           const StepArgs<NP, NS, MS>& args) {
   using G = TileGeo<NP, W>;
   constexpr int T = G::T, LB = G::LB, EPL = 1;
-  constexpr int H = MS * NS;     // dependency cone: one element per stage
+  // dependency cone: one element per stage (+1 with the jump record: the final state's
+  // jumps need the output elements' neighbours after the last stage)
+  constexpr int H = MS * NS + (REC ? 1 : 0);
   constexpr int TE = T - 2 * H;  // output elements per tile (even)
   static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
@@ -81,8 +93,8 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
     // path into SGPR spills.
     using SArgs = StepArgs<NP, NS, MS>;
     const double* ka = reinterpret_cast<const double*>(
-        kernarg_tail<decltype(&k_step<NP, NS, UNI, W, MS>), SArgs>() + offsetof(SArgs, uin));
-    if (lane < MS * NS) lds[CB + lane] = ka[lane];
+        kernarg_tail<decltype(&k_step<NP, NS, UNI, W, MS, REC>), SArgs>() + offsetof(SArgs, uin));
+    if (lane <= MS * NS) lds[CB + lane] = ka[lane];
   }
   __syncthreads();
   double ev[EPL][NE], od[EPL][NO];  // the element state in even/odd coordinates
@@ -95,6 +107,18 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
     E[m] = elem_info<H, T, EDGE>(e0, el, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= E[m].inrange ? scale[E[m].kl] : 0.0;
+    if constexpr (REC) {
+      // The launch's input state u^{n0} (record n0-1) from its nodal values in the staged
+      // image -- the values a snapshot holds; the even/odd round trip ev_0 + od_0 can differ
+      // from them in the last bit.  Inflow at t_{n0} = the first stage's, own node at the end.
+      if (args.n0 >= 1 && E[m].valid) {
+        const double* us = lds + pf.off + el * NP;
+        const double uL = (EDGE && E[m].first) ? lds[CB] : us[-1];
+        const double uR = (EDGE && E[m].last) ? us[NP - 1] : us[NP];
+        const double du0 = us[0] - uL, du1 = us[NP - 1] - uR;
+        *jump_slot(snap, args.n0 - 1, args.ktot, E[m].e) = double2{du0 - du1, du0 + du1};
+      }
+    }
   }
 
   double re[EPL][NE], ro[EPL][NO];
@@ -155,6 +179,12 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
         // only uR - uL and uL + uR remain.
         const double uL = lds[iL], uR = lds[iR];
         const double dlt = uR - uL, sig = -(uL + uR);
+        if constexpr (REC) {  // u^{n0+st}'s jumps (record n0+st-1), stage 0 of its step
+          if (s == 0 && st >= 1 && E[m].valid) {
+            const double du0 = u0[m] - uL, du1 = uN[m] - uR;
+            *jump_slot(snap, args.n0 + st - 1, args.ktot, E[m].e) = double2{du0 - du1, du0 + du1};
+          }
+        }
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
           if constexpr (UNI) {  // r = A_s r + dt*L u, dt*2/h folded into the operator
@@ -195,39 +225,56 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
       continue;
     }
 #endif
-    if (snap != nullptr || st == MS - 1) {
+    if (REC && st == MS - 1 && args.jend) {
+      // The sweep's final state u^{n0+MS}: one more face exchange (the buffer parity of the
+      // stage after the last) for its jumps, record n0+MS-1; inflow at t_{n0+MS}.
+      const int fL = G::kFB + ((MS * NS) & 1) * 2 * (T + 2), fR = fL + (T + 2);
+      const int el = lane;
+      const double u0 = ev[0][0] + od[0][0], uN = ev[0][0] - od[0][0];
+      lds[fL + el + 1] = u0;
+      lds[fR + el + 1] = uN;
+      __syncthreads();
+      const int iL = EDGE && E[0].first ? CB + MS * NS : fR + el;
+      const int iR = EDGE && E[0].last ? fR + el + 1 : fL + el + 2;
+      if (E[0].valid) {
+        const double du0 = u0 - lds[iL], du1 = uN - lds[iR];
+        *jump_slot(snap, args.n0 + MS - 1, args.ktot, E[0].e) = double2{du0 - du1, du0 + du1};
+      }
+    }
+    if ((!REC && snap != nullptr) || st == MS - 1) {
       // The image's last readers (staging reads, the previous step's store) are at least
       // one stage barrier behind; the faces live elsewhere.
       stage_out<NP, W, H>(lds, ev, od, false);
       __syncthreads();
       if constexpr (EDGE) {
-        if (snap != nullptr) store_run<LB>(snap + st * args.stride, o0, count, lds);
+        if (!REC && snap != nullptr) store_run<LB>(snap + st * args.stride, o0, count, lds);
         if (st == MS - 1 && last != nullptr) store_run<LB>(last, o0, count, lds);
       } else {
-        if (snap != nullptr) store_full<TE * NP, LB>(snap + st * args.stride, o0, lds);
+        if (!REC && snap != nullptr) store_full<TE * NP, LB>(snap + st * args.stride, o0, lds);
         if (st == MS - 1 && last != nullptr) store_full<TE * NP, LB>(last, o0, lds);
       }
     }
   }
 }
 
-template <int NP, int NS, bool UNI, int W, int MS>
+template <int NP, int NS, bool UNI, int W, int MS, bool REC>
 __global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* __restrict__ uin,
                                                      double* __restrict__ snap,
                                                      double* __restrict__ last,
                                                      const double* __restrict__ scale,
                                                      StepArgs<NP, NS, MS> args) {
   using G = TileGeo<NP, W>;
-  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * NS];
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * NS + 1];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
 #ifdef DG_SETPRIO_ODD  // experiment: desynchronise co-resident workgroups (MI355X_MICROARCH.md)
   if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
 #endif
-  const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
+  constexpr int H = MS * NS + (REC ? 1 : 0);
+  const int64_t e0 = tile * (G::T - 2 * H) - H;
   if (edge_tile(e0, G::T, args.ktot, args.K))
-    step_tile<NP, NS, UNI, W, MS, true>(lds, tile, uin, snap, last, scale, args);
+    step_tile<NP, NS, UNI, W, MS, REC, true>(lds, tile, uin, snap, last, scale, args);
   else
-    step_tile<NP, NS, UNI, W, MS, false>(lds, tile, uin, snap, last, scale, args);
+    step_tile<NP, NS, UNI, W, MS, REC, false>(lds, tile, uin, snap, last, scale, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -240,7 +287,7 @@ __global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* 
 // Indicator: eta += dt * sum_i w_i * s*(L0_i du0 + L1_i du1), with L0.w = le.we + lo.wo and
 // L1.w = -le.we + lo.wo.  The next snapshot tile is prefetched during each step's stages.
 // ---------------------------------------------------------------------------
-template <int NP, int NS, bool UNI, int W, int MS, bool EDGE>
+template <int NP, int NS, bool UNI, int W, int MS, bool REC, bool EDGE>
 __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
                                          const double* __restrict__ win,
                                          double* __restrict__ wout,
@@ -260,13 +307,22 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 
   constexpr int CB = G::kLds;  // lds[CB + st] = inflow value at t_{n+st+1}; lds[CB + MS] = 0
   TileRegs<NP, W> pw, pu;
+  // REC: the jumps of u^{n0+st+1} (record n0+st), one 16-byte load per lane and step,
+  // prefetched a step ahead
+  const bool jin = REC && e0 + lane >= 0 && e0 + lane < args.ktot;
+  double2 jn{0.0, 0.0};
   tile_issue<NP, W, EDGE>(win, e0, nd, pw);
-  tile_issue<NP, W, EDGE>(snap + (MS - 1) * args.stride, e0, nd, pu);
+  if constexpr (REC) {
+    if (jin) jn = *jump_slot(const_cast<double*>(snap), args.n0 + MS - 1, args.ktot, e0 + lane);
+  } else {
+    tile_issue<NP, W, EDGE>(snap + (MS - 1) * args.stride, e0, nd, pu);
+  }
   tile_commit<NP, W>(pw, lds);
   if constexpr (EDGE) {
     using AArgs = AdjArgs<NP, MS>;
     const double* ka = reinterpret_cast<const double*>(  // see step_tile
-        kernarg_tail<decltype(&k_adj<NP, NS, UNI, W, MS>), AArgs>() + offsetof(AArgs, uin_res));
+        kernarg_tail<decltype(&k_adj<NP, NS, UNI, W, MS, REC>), AArgs>() +
+        offsetof(AArgs, uin_res));
     if (lane < MS) lds[CB + lane] = ka[lane];
     if (lane == MS) lds[CB + MS] = 0.0;
   }
@@ -296,15 +352,31 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 
 #pragma unroll
   for (int st = MS - 1; st >= 0; --st) {
+    if constexpr (REC) {
+      // no snapshot: the record's jumps replace the staged tile's neighbour faces
+      const double2 jc = jn;
+      if (st > 0 && jin)
+        jn = *jump_slot(const_cast<double*>(snap), args.n0 + st - 1, args.ktot, e0 + lane);
+      if (args.has_eta) {
+        double pe = 0.0, po = 0.0;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[0][k], pe);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[0][k], po);
+        double c = fma(jc.x, pe, jc.y * po);
+        if constexpr (!UNI) c *= sc[0];
+        eacc[0] += c;
+      }
+    }
     // The w tile's readers must be done before the first snapshot overwrites the image;
     // later snapshots follow 5 stage barriers after the previous one's reads.
-    if (st == MS - 1) __syncthreads();
-    tile_commit<NP, W>(pu, lds);
-    const int off = pu.off;
-    __syncthreads();
-    if (st > 0) tile_issue<NP, W, EDGE>(snap + (st - 1) * args.stride, e0, nd, pu);
+    if (!REC && st == MS - 1) __syncthreads();
+    if constexpr (!REC) tile_commit<NP, W>(pu, lds);
+    const int off = REC ? 0 : pu.off;
+    if constexpr (!REC) __syncthreads();
+    if (!REC && st > 0) tile_issue<NP, W, EDGE>(snap + (st - 1) * args.stride, e0, nd, pu);
 #pragma unroll
-    for (int m = 0; m < EPL; ++m) {
+    for (int m = 0; m < (REC ? 0 : EPL); ++m) {
       const int el = m * LB + lane;
       const double* us = lds + off + el * NP;
       if (args.src[st] != 0.0) {  // functional source (dual coordinates)
@@ -434,7 +506,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
   }
 }
 
-template <int NP, int NS, bool UNI, int W, int MS>
+template <int NP, int NS, bool UNI, int W, int MS, bool REC>
 __global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(const double* __restrict__ win,
                                                     double* __restrict__ wout,
                                                     const double* __restrict__ snap,
@@ -449,9 +521,9 @@ __global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(co
 #endif
   const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
   if (edge_tile(e0, G::T, args.ktot, args.K))
-    adj_tile<NP, NS, UNI, W, MS, true>(lds, tile, win, wout, snap, eta, scale, args);
+    adj_tile<NP, NS, UNI, W, MS, REC, true>(lds, tile, win, wout, snap, eta, scale, args);
   else
-    adj_tile<NP, NS, UNI, W, MS, false>(lds, tile, win, wout, snap, eta, scale, args);
+    adj_tile<NP, NS, UNI, W, MS, REC, false>(lds, tile, win, wout, snap, eta, scale, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -777,34 +849,43 @@ template <int NP> LimArgs<NP> make_lim(const dg_plan* p) {
   return la;
 }
 
-template <int NP, int NS, int W, int MS>
+// Jump-record sweeps (REC): `snap` is the record, `rec` = {n0, jend} (see jump_slot).
+struct RecPos {
+  int64_t n0 = 0;
+  bool jend = false;
+};
+
+template <int NP, int NS, int W, int MS, bool REC = false>
 int launch_step_e(const dg_plan* p, const double* in, double* snap, double* last,
-                  const double* times, double dt, hipStream_t st) {
+                  const double* times, double dt, hipStream_t st, RecPos rec = {}) {
   StepArgs<NP, NS, MS> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
   a.sc = dt;  // non-uniform meshes multiply by scale[k] in the kernel
   for (int m = 0; m < MS; ++m)
     for (int s = 0; s < NS; ++s) a.uin[m * NS + s] = inflow_value(p, times[m] + RK<NS>::C(s) * dt);
+  a.uin[MS * NS] = inflow_value(p, times[MS]);  // t_{n0+MS} (the record's final exchange)
   a.ktot = p->ktot;
   a.stride = p->ktot * NP;
+  a.n0 = rec.n0;
   a.K = int32_t(p->K);
   a.xcd = p->xcd_order;
-  constexpr int TE = kBlock * W - 2 * MS * NS;
+  a.jend = rec.jend ? 1 : 0;
+  constexpr int TE = kBlock * W - 2 * (MS * NS + (REC ? 1 : 0));
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_step<NP, NS, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
-                       snap, last, p->d_scale, a);
+    hipLaunchKernelGGL((k_step<NP, NS, true, W, MS, REC>), dim3(grid), dim3(kBlock * W), 0, st,
+                       in, snap, last, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_step<NP, NS, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
-                       snap, last, p->d_scale, a);
+    hipLaunchKernelGGL((k_step<NP, NS, false, W, MS, REC>), dim3(grid), dim3(kBlock * W), 0, st,
+                       in, snap, last, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-template <int NP, int NS, int W, int MS>
+template <int NP, int NS, int W, int MS, bool REC = false>
 int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double* snap,
                  double* eta, int eta_mode, const double* t_next, const double* src, double dt,
-                 hipStream_t st) {
+                 hipStream_t st, int64_t n0 = 0) {
   AdjArgs<NP, MS> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
   a.sc = dt;
@@ -814,17 +895,18 @@ int launch_adj_e(const dg_plan* p, const double* win, double* wout, const double
   }
   a.ktot = p->ktot;
   a.stride = p->ktot * NP;
+  a.n0 = n0;
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr ? (eta_mode | kEtaOn) : 0;
   a.xcd = p->xcd_order;
   constexpr int TE = kBlock * W - 2 * MS * NS;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_adj<NP, NS, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
-                       wout, snap, eta, p->d_scale, a);
+    hipLaunchKernelGGL((k_adj<NP, NS, true, W, MS, REC>), dim3(grid), dim3(kBlock * W), 0, st,
+                       win, wout, snap, eta, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_adj<NP, NS, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
-                       wout, snap, eta, p->d_scale, a);
+    hipLaunchKernelGGL((k_adj<NP, NS, false, W, MS, REC>), dim3(grid), dim3(kBlock * W), 0, st,
+                       win, wout, snap, eta, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
@@ -896,6 +978,44 @@ int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const 
   return rc;
 }
 
+// Jump-record launches: LSERK4 (NS = 5) on the workgroup tiles, the plan's tile width and
+// steps per launch (the 8-step shape on 512-element tiles; Np = 9 at most 2 steps).
+template <int NP>
+int launch_step_rec_t(const dg_plan* p, int ms, const double* in, double* rec, double* last,
+                      const double* times, double dt, hipStream_t st, RecPos pos) {
+  const bool w2 = p->tile_width == 2;
+  if constexpr (NP <= 8) {
+    if (ms == 8) return launch_step_e<NP, 5, 2, 8, true>(p, in, rec, last, times, dt, st, pos);
+    if (ms == 4 && w2) return launch_step_e<NP, 5, 2, 4, true>(p, in, rec, last, times, dt, st, pos);
+    if (ms == 4) return launch_step_e<NP, 5, 1, 4, true>(p, in, rec, last, times, dt, st, pos);
+  }
+  if (ms == 2 && w2) return launch_step_e<NP, 5, 2, 2, true>(p, in, rec, last, times, dt, st, pos);
+  if (ms == 2) return launch_step_e<NP, 5, 1, 2, true>(p, in, rec, last, times, dt, st, pos);
+  if (w2) return launch_step_e<NP, 5, 2, 1, true>(p, in, rec, last, times, dt, st, pos);
+  return launch_step_e<NP, 5, 1, 1, true>(p, in, rec, last, times, dt, st, pos);
+}
+
+template <int NP>
+int launch_adj_rec_t(const dg_plan* p, int ms, const double* win, double* wout, const double* rec,
+                     double* eta, int em, const double* t_next, const double* src, double dt,
+                     hipStream_t st, int64_t n0) {
+  const bool w2 = p->tile_width == 2;
+  if constexpr (NP <= 8) {
+    if (ms == 8)
+      return launch_adj_e<NP, 5, 2, 8, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
+    if (ms == 4 && w2)
+      return launch_adj_e<NP, 5, 2, 4, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
+    if (ms == 4)
+      return launch_adj_e<NP, 5, 1, 4, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
+  }
+  if (ms == 2 && w2)
+    return launch_adj_e<NP, 5, 2, 2, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
+  if (ms == 2)
+    return launch_adj_e<NP, 5, 1, 2, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
+  if (w2) return launch_adj_e<NP, 5, 2, 1, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
+  return launch_adj_e<NP, 5, 1, 1, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
+}
+
 // Steps per launch the plan's shape allows: 8 only with 512-element tiles (the cone is
 // 8*NS elements per side) and Np <= 8; at Np = 9 at most 2 (hipcc/ROCm 7.2 fails
 // instruction selection for the 4-step shape there).
@@ -905,6 +1025,15 @@ inline int effective_msteps(const dg_plan* p) {
   if (m == 8 && p->lane_elems == 2) m = 4;  // 128-element wave tiles: cone too wide
   if (p->NP > 8 && m > 2) m = 2;
   return m;
+}
+
+// Steps per launch of a jump-record sweep: the plan's setting on the workgroup tiles.
+inline int chunk_rec(const dg_plan* p, int left) {
+  int m = p->msteps;
+  if (m == 8 && p->tile_width != 2) m = 4;
+  if (p->NP > 8 && m > 2) m = 2;
+  while (m > left) m >>= 1;
+  return m < 1 ? 1 : m;
 }
 
 // Steps per launch for the next chunk of `left` steps (greedy over {4, 2, 1}, capped by
@@ -1281,6 +1410,88 @@ int dg_lserk4_adj_ex(dg_plan* p, double* w, const double* snapshots, double t0, 
                        snapshots, nsteps > 0 ? src_coef : 0.0, w, field);
     HIP_TRY(hipGetLastError());
   }
+  return DG_OK;
+}
+
+int dg_lserk4_fwd_rec(dg_plan* p, const double* u0, double* uN, double t0, double dt,
+                      int nsteps, double* jumps, void* stream) {
+  if (!p || !u0 || !uN || (!jumps && nsteps > 0)) return fail(DG_ERR_ARG, "null argument");
+  if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
+  if (p->nonlinear() || p->nstages != 5)
+    return fail(DG_ERR_ARG, "the jump record is the linear LSERK4 sweep's (use snapshots)");
+  if (reinterpret_cast<uintptr_t>(jumps) % 16 != 0)
+    return fail(DG_ERR_ARG, "the jump record must be 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t field = p->ktot * p->NP;
+  if (nsteps == 0) {
+    if (uN != u0)
+      HIP_TRY(hipMemcpyAsync(uN, u0, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
+    return DG_OK;
+  }
+  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt (One_code.mlx:139)
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  // Launch l reads in_l and writes the next state: the last launch lands in uN, the others
+  // alternate between the two plan scratch fields (a launch never writes its own input, so
+  // u0 == uN is allowed and u0 is otherwise left untouched).
+  int launches = 0;
+  for (int n = 0; n < nsteps; n += chunk_rec(p, nsteps - n)) ++launches;
+  const double* in = u0;
+  int l = 0;
+  for (int n = 0; n < nsteps; ++l) {
+    const int m = chunk_rec(p, nsteps - n);
+    const bool final = (n + m == nsteps);
+    double* out = (final && in != uN) ? uN : ((l % 2 == 0) ? p->d_scratch : p->d_scratch2);
+    RecPos pos;
+    pos.n0 = n;
+    pos.jend = final;
+    int rc = DG_OK;
+    DG_DISPATCH_NP(p->NP, rc = launch_step_rec_t<NP>(p, m, in, jumps, out, &tn[n], dt, st, pos));
+    if (rc) return rc;
+    in = out;
+    n += m;
+  }
+  if (in != uN)  // (a one-launch in-place sweep went through scratch)
+    HIP_TRY(hipMemcpyAsync(uN, in, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
+  return DG_OK;
+}
+
+int dg_lserk4_adj_rec(dg_plan* p, double* w, const double* jumps, double t0, double dt,
+                      int nsteps, double* eta, int flags, void* stream) {
+  if (!p || !w || (!jumps && eta && nsteps > 0)) return fail(DG_ERR_ARG, "null argument");
+  if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
+  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS)) return fail(DG_ERR_ARG, "unknown flags");
+  if (p->nonlinear() || p->nstages != 5)
+    return fail(DG_ERR_ARG, "the jump record is the linear LSERK4 sweep's (use snapshots)");
+  if (reinterpret_cast<uintptr_t>(jumps) % 16 != 0)
+    return fail(DG_ERR_ARG, "the jump record must be 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (eta != nullptr && nsteps == 0 && (flags & DG_ADJ_ETA_ASSIGN))
+    HIP_TRY(hipMemsetAsync(eta, 0, sizeof(double) * p->ktot, st));
+  const int64_t field = p->ktot * p->NP;
+  std::vector<double> tn(size_t(nsteps) + 1), src(size_t(nsteps) + 1, 0.0);
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  int launches = 0;
+  for (int n = nsteps; n > 0; n -= chunk_rec(p, n)) ++launches;
+  int l = 0;
+  const double* in = w;
+  for (int n = nsteps; n > 0; ++l) {  // this launch covers steps n-m .. n-1
+    const int m = chunk_rec(p, n);
+    const int n0 = n - m;
+    double* out = (l == launches - 1 && launches > 1)
+                      ? w : ((l % 2 == 0) ? p->d_scratch : p->d_scratch2);
+    const int em = ((l == 0 && (flags & DG_ADJ_ETA_ASSIGN)) ? kEtaAssign : 0) |
+                   ((n0 == 0 && (flags & DG_ADJ_ETA_ABS)) ? kEtaAbs : 0);
+    int rc = DG_OK;
+    DG_DISPATCH_NP(p->NP, rc = launch_adj_rec_t<NP>(p, m, in, out, jumps, eta, em, &tn[n0 + 1],
+                                                    &src[n0 + 1], dt, st, n0));
+    if (rc) return rc;
+    in = out;
+    n = n0;
+  }
+  if (in != w)
+    HIP_TRY(hipMemcpyAsync(w, in, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
   return DG_OK;
 }
 

@@ -377,6 +377,7 @@ template <int NP> struct NLAdjArgs {
   double sc;
   double fin[6];   // inflow flux at the 5 stage times of step n, then at t_{n+1} (residual)
   double src;      // functional source coefficient of node n+1
+  double qoe_h[EOArgs<NP>::NO * EOArgs<NP>::NE];  // Burgers: op.Qoe / 2 for the recompute (HQ)
   int64_t ktot;
   int32_t K;
   int32_t has_eta;  // kEta* bits
@@ -471,6 +472,13 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   double se[5][NE], so[5][NO];
   int dcodes = 0;
   {
+    // the recompute's operator: the Burgers even flux doubled against Qoe/2 (flux_eo HQ);
+    // the reverse pass keeps Qoe
+    EOArgs<NP> oph = args.op;
+    if constexpr (BURG) {
+#pragma unroll
+      for (int k = 0; k < NO * NE; ++k) oph.Qoe[k] = args.qoe_h[k];
+    }
     double re[NE], ro[NO];
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
@@ -485,8 +493,8 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 #pragma unroll
         for (int k = 0; k < NO; ++k) lds[SE1 + (NE + k) * T + lane] = od[k];
       }
-      const int c = nl_stage<NP, BURG, LIM, UNI, EDGE, KNOWN, W>(
-          lds, lane, s, s & 1, CB + s, E, sc, args.op, args.lc, args.lc, ev, od, re, ro,
+      const int c = nl_stage<NP, BURG, LIM, UNI, EDGE, KNOWN, W, BURG>(
+          lds, lane, s, s & 1, CB + s, E, sc, oph, args.lc, args.lc, ev, od, re, ro,
           (kcode >> (3 * s)) & 7, ((wg >> (3 * s)) & 4) != 0);
       if constexpr (LIM) dcodes |= c << (3 * s);
     }
@@ -821,6 +829,7 @@ int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const doubl
                   hipStream_t st) {
   NLAdjArgs<NP> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : dt, &a.op);  // see launch_step_nl
+  for (int k = 0; k < EOArgs<NP>::NO * EOArgs<NP>::NE; ++k) a.qoe_h[k] = 0.5 * a.op.Qoe[k];
   a.lc = make_lim_eo<NP>(p);
   a.sc = 1.0;
   for (int s = 0; s < 5; ++s) a.fin[s] = flux_value(BURG, inflow_value(p, t_n + RK<5>::C(s) * dt));

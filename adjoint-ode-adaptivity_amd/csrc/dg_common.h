@@ -159,12 +159,14 @@ template <int NP> struct EOArgs {
 // Arguments of a launch that advances MS time steps of NS stages each.
 template <int NP, int NS, int MS> struct StepArgs {
   EOArgs<NP> op;
-  double sc;            // dt (non-uniform meshes multiply by scale[k]; uniform: folded in op)
-  double uin[MS * NS];  // inflow value at each stage time
-  int64_t ktot;         // batch * K elements
-  int64_t stride;       // doubles between consecutive snapshots
-  int32_t K;            // elements per trajectory
-  int32_t xcd;          // XCD-aware tile order (speed only)
+  double sc;                // dt (non-uniform meshes multiply by scale[k]; uniform: folded in op)
+  double uin[MS * NS + 1];  // inflow value at each stage time, then at t_{n0+MS}
+  int64_t ktot;             // batch * K elements
+  int64_t stride;           // doubles between consecutive snapshots
+  int64_t n0;               // jump record: global index of the launch's first step
+  int32_t K;                // elements per trajectory
+  int32_t xcd;              // XCD-aware tile order (speed only)
+  int32_t jend;             // jump record: the launch ends the sweep (record u^{n0+MS} too)
 };
 
 template <int NP, int MS> struct AdjArgs {
@@ -174,6 +176,7 @@ template <int NP, int MS> struct AdjArgs {
   double src[MS];      // functional source coefficient for node n+st+1
   int64_t ktot;
   int64_t stride;      // doubles between consecutive snapshots
+  int64_t n0;          // jump record: global index of the launch's first step
   int32_t K;
   int32_t has_eta;     // kEta* bits
   int32_t xcd;         // XCD-aware tile order (speed only)

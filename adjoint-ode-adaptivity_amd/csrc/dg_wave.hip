@@ -224,6 +224,9 @@ int launch_wstep_e(const dg_plan* p, const double* in, double* snap, double* las
   a.stride = p->ktot * NP;
   a.K = int32_t(p->K);
   a.xcd = p->xcd_order;
+  a.uin[MS * 5] = 0.0;  // (no jump record on the wave path)
+  a.n0 = 0;
+  a.jend = 0;
   constexpr int TE = WaveGeo<NP, E, MS, 5>::TE;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)

@@ -49,21 +49,38 @@ class EnsembleSweep:
   All work is enqueued on torch's current stream; ``run`` does not synchronise.
   """
 
+  RECORDS = ("jumps", "snapshots")
+
   def __init__(self, mesh, ic_indices, nsteps, dt, a=2 * np.pi, inflow="a", seed_base=0,
-               params=None):
+               params=None, record="jumps"):
     self.ic_indices = list(ic_indices)
     self.batch = len(self.ic_indices)
     if self.batch < 1:
       raise ValueError("a rank needs at least one IC")
+    if record not in self.RECORDS:
+      raise ValueError(f"record must be one of {self.RECORDS}, got {record!r}")
+    self.record = record
     self.nsteps, self.dt = int(nsteps), float(dt)
     self.op = DGAdvection1D(mesh, a=a, batch=self.batch, inflow=inflow)
     amp, freq, phase = params if params is not None else ic_params(self.ic_indices, seed_base)
-    self.snaps = self.op.new_field(self.nsteps + 1)
-    # u^0 lives in snapshot 0; the forward sweep with u aliasing it leaves it untouched.
-    self.op.init_sine(amp, freq, phase, out=self.snaps[0])
-    # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
-    # place on snapshot N (the library allows that alias) and leaves dJ/du^0 there.
-    self.w = self.snaps[self.nsteps]
+    if record == "jumps":
+      # The snapshot-free pair (dg_lserk4_fwd_rec / dg_lserk4_adj_rec): the forward keeps
+      # per element and step only the two face jumps the indicator needs (16 B instead of
+      # 8 Np B); w, eta and the refine decision are bit-identical to the snapshot pair's.
+      self.u0 = self.op.new_field()
+      self.op.init_sine(amp, freq, phase, out=self.u0)
+      self.jumps = self.op.new_jumps(self.nsteps)
+      # J = |u^N|^2 / 2: the forward writes u^N into w, the adjoint's terminal value
+      self.w = self.op.new_field()
+      self.snaps = None
+    else:
+      self.snaps = self.op.new_field(self.nsteps + 1)
+      # u^0 lives in snapshot 0; the forward sweep with u aliasing it leaves it untouched.
+      self.op.init_sine(amp, freq, phase, out=self.snaps[0])
+      self.u0 = self.snaps[0]
+      # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
+      # place on snapshot N (the library allows that alias) and leaves dJ/du^0 there.
+      self.w = self.snaps[self.nsteps]
     # per-IC |eta| rows; the adjoint's first launch assigns them (DG_ADJ_ETA_ASSIGN), so
     # they need no zero fill
     self.eta = torch.zeros(self.op.ktot, dtype=torch.float64, device=self.op.device)
@@ -76,7 +93,10 @@ class EnsembleSweep:
     return 2 * self.op.Np * self.op.ktot * self.nsteps
 
   def forward(self):
-    self.op.forward(self.snaps[0], 0.0, self.dt, self.nsteps, self.snaps)
+    if self.record == "jumps":
+      self.op.forward_rec(self.u0, 0.0, self.dt, self.nsteps, self.jumps, out=self.w)
+    else:
+      self.op.forward(self.snaps[0], 0.0, self.dt, self.nsteps, self.snaps)
 
   def adjoint(self):
     self.run_adjoint()
@@ -84,8 +104,12 @@ class EnsembleSweep:
   def run_adjoint(self):
     """The adjoint kernels: w^N -> w^0 in place and eta = |DWR| per IC row (assigned, not
     accumulated: no zero fill needed)."""
-    self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta,
-                    eta_assign=True, eta_abs=True)
+    if self.record == "jumps":
+      self.op.adjoint_rec(self.w, self.jumps, 0.0, self.dt, self.nsteps, eta=self.eta,
+                          eta_assign=True, eta_abs=True)
+    else:
+      self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta,
+                      eta_assign=True, eta_abs=True)
 
   def capture(self):
     """Capture the forward and adjoint sweeps as two HIP graphs (replayed by

@@ -248,6 +248,36 @@ class DGAdvection1D:
     _lib.check(rc, "dg_lserk4_adj_ex")
     return w, eta
 
+  # --- snapshot-free sweep pair (linear LSERK4 plans, terminal functionals) ---
+  def new_jumps(self, nsteps):
+    """A jump record for an ``nsteps`` sweep: (nsteps, batch*K, 2) float64."""
+    return torch.empty((int(nsteps), self.ktot, 2), dtype=torch.float64, device=self.device)
+
+  def _jumps(self, jumps, nsteps):
+    return self._field(jumps, "jumps", 2 * int(nsteps) * self.ktot)
+
+  def forward_rec(self, u0, t0, dt, nsteps, jumps, out=None):
+    """``nsteps`` LSERK4 steps from u0 into ``out`` (default: in place on u0), recording
+    per element and step the two interelement jumps of each state u^1..u^nsteps instead of
+    the states (dg_lserk4_fwd_rec: 16 bytes per element-step for 8*Np).  With
+    ``adjoint_rec`` this is the snapshot sweep pair with src_coef = 0, bit for bit."""
+    out = u0 if out is None else out
+    rc = self._lib.dg_lserk4_fwd_rec(self._plan, self._field(u0, "u0"), self._field(out, "out"),
+                                     float(t0), float(dt), int(nsteps),
+                                     self._jumps(jumps, nsteps), _stream(self.device))
+    _lib.check(rc, "dg_lserk4_fwd_rec")
+    return out
+
+  def adjoint_rec(self, w, jumps, t0, dt, nsteps, eta=None, eta_assign=False, eta_abs=False):
+    """``adjoint`` (src_coef = 0) from the record ``forward_rec`` wrote for this sweep."""
+    eta_p = None if eta is None else self._field(eta, "eta", self.ktot)
+    flags = (_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) | (_lib.DG_ADJ_ETA_ABS if eta_abs else 0)
+    rc = self._lib.dg_lserk4_adj_rec(self._plan, self._field(w, "w"), self._jumps(jumps, nsteps),
+                                     float(t0), float(dt), int(nsteps), eta_p, int(flags),
+                                     _stream(self.device))
+    _lib.check(rc, "dg_lserk4_adj_rec")
+    return w, eta
+
   def slope_limit(self, u, out=None, ids=None):
     """SlopeLimitN(u) (utils/SlopeLimitN.m:1-33); ids (int32, batch*K) marks limited cells."""
     out = torch.empty_like(u) if out is None else out

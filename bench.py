@@ -1,6 +1,7 @@
 """Benchmark: DOF-updates/s of the 1D DG advection forward + adjoint sweep (BASELINE.json).
 
-One bench step = one forward sweep of --nsteps fused LSERK4 steps (snapshots stored),
+One bench step = one forward sweep of --nsteps fused LSERK4 steps (recording for the
+indicator the two face jumps per element and step, or with --record snapshots the states),
 one adjoint sweep of --nsteps reverse steps writing each trajectory's dual-weighted
 residual magnitude |eta| (DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS: no zero fill, no extra pass),
 the per-rank indicator reduction, the cross-rank rank-ordered sum (all-to-all + all-gather)
@@ -73,6 +74,10 @@ def parse(argv=None):
   p.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                  help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo stages the "
                       "exchange through host memory: for tests with several ranks on one GPU)")
+  p.add_argument("--record", default="jumps", choices=("jumps", "snapshots"),
+                 help="what the forward sweep keeps for the indicator: the two face jumps per "
+                      "element and step (dg_lserk4_fwd_rec, default) or full snapshots "
+                      "(dg_lserk4_fwd); results are bit-identical")
   p.add_argument("--no-cpu-baseline", action="store_true")
   p.add_argument("--cpu-steps", type=int, default=12, help="time steps of the CPU sample")
   p.add_argument("--graph", action="store_true",
@@ -448,7 +453,7 @@ def main(argv=None):
     params = ((np.array([1.0]), np.array([1.0]), np.array([0.0])) if rank == 0
               else ens.ic_params([rank]))
     n_total = world
-  sweep = ens.EnsembleSweep(mesh, ics, nsteps, dt, params=params)
+  sweep = ens.EnsembleSweep(mesh, ics, nsteps, dt, params=params, record=args.record)
   reducer = ens.DeviceReducer(sweep.op)  # argmax + value + non-finite count on the device
   if args.graph:
     sweep.capture()  # each sweep becomes one HIP graph launch
@@ -508,13 +513,21 @@ def main(argv=None):
              for i in range(len(evs))]
   fwd_launch_us, adj_launch_us = float(np.mean(fwd_us)), float(np.mean(adj_us))
   # Algorithmic bytes of a launch of m fused steps:
-  #   forward: read u^n once, write the m snapshots u^{n+1..n+m}:  (8 + 8 m) B per DOF
-  #   adjoint: read w^{n+m}, read the m snapshots, write w^n: (16 + 8 m) B per DOF,
-  #            plus the indicator read-modify-write, 16 B per element.
+  #   snapshots: forward reads u^n once and writes the m snapshots u^{n+1..n+m}: (8 + 8 m) B
+  #     per DOF; the adjoint reads w^{n+m} and the m snapshots and writes w^n: (16 + 8 m) B
+  #     per DOF, plus the indicator read-modify-write, 16 B per element;
+  #   jumps: forward reads u^n, writes u^{n+m} and m jump pairs: 16 B per DOF + 16 m B per
+  #     element; the adjoint reads w^{n+m} and m jump pairs, writes w^n, updates eta:
+  #     16 B per DOF + (16 m + 16) B per element.
   # A sweep's launches may differ in m (e.g. 8 + 8 + 4 at 20 steps); the per-launch figures
   # are the sweep's averages: achieved = sweep bytes / sweep time.
-  fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in chunks]))
-  adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
+  if args.record == "jumps":
+    fwd_bytes = float(np.mean([(16.0 * Np + 16.0 * m) * ktot for m in chunks]))
+    adj_bytes = float(np.mean([(16.0 * Np + 16.0 * m + 16.0) * ktot for m in chunks]))
+  else:
+    fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in chunks]))
+    adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
+  rec_tag = ",jumps" if args.record == "jumps" else ""
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
@@ -523,7 +536,8 @@ def main(argv=None):
       with open(PROFILE_TRAFFIC) as f:
         tr = json.load(f)
       if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
-          and tr.get("steps_per_launch") == ms):
+          and tr.get("steps_per_launch") == ms
+          and tr.get("record", "snapshots") == args.record):
         traffic = tr.get("adj_bytes_per_launch")
         traffic_src = tr.get("source")
     except (OSError, ValueError):
@@ -559,18 +573,19 @@ def main(argv=None):
       "data": "synthetic (u0 = sin(2 pi x) on rank 0, SURVEY 8d sine-family ICs on other ranks)",
       "config": {"workload": (f"config {'4' if args.ics > 0 else '2'}: 1D DG advection N={N} "
                               f"K={K} x {n_total} trajectories, LSERK4 fwd+adj {nsteps}+{nsteps} "
-                              f"steps/sweep + DWR indicator + refine argmax"),
+                              f"steps/sweep + DWR indicator + refine argmax; indicator "
+                              f"record: {args.record}"),
                  "N": N, "K": K, "nsteps_per_sweep": nsteps, "trajectories": n_total,
                  "trajectories_per_gpu": sweep.batch, "parallelism": f"ensemble-dp{world}",
-                 "per_ic_gather": bool(args.gather_ics)},
+                 "per_ic_gather": bool(args.gather_ics), "record": args.record},
       "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                   "kernel": f"k_adj<{Np},5,uniform,{sweep.op.tile_width},{ms}> ({ms} reverse steps + DWR per launch)",
+                   "kernel": f"k_adj<{Np},5,uniform,{sweep.op.tile_width},{ms}{rec_tag}> ({ms} reverse steps + DWR per launch)",
                    "launch_us": adj_launch_us, "launch_us_stats": stats(adj_us),
                    "algorithmic_bytes": adj_bytes, "traffic_source": traffic_src},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_gbs / HBM_PEAK_GBS,
-                       "kernel": f"k_step<{Np},5,uniform,{sweep.op.tile_width},{ms}> ({ms} steps per launch)",
+                       "kernel": f"k_step<{Np},5,uniform,{sweep.op.tile_width},{ms}{rec_tag}> ({ms} steps per launch)",
                        "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
       "step_ms_stats": stats(step_ms),

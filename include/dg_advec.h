@@ -180,6 +180,24 @@ int dg_lserk4_adj_ex(dg_plan* plan, double* w, const double* snapshots, double t
                      int nsteps, double src_coef, double* eta, int flags,
                      const uint16_t* decisions, void* stream);
 
+/* Snapshot-free sweep pair (linear flux, LSERK4).  For the linear advection operator the
+ * adjoint S^T does not depend on the state, and the indicator needs of each u^n only the two
+ * interelement jumps per element (R = LIFT*(Fscale.*du), utils/AdvecRHS1D.m:19: du0 at the
+ * left face, du1 at the right face, inflow / outflow rules as in AdvecRHS1D).  The forward
+ * records them instead of the states: 16 bytes per element and step where a snapshot takes
+ * 8*Np.  w, eta and the final state are bit-identical to the dg_lserk4_fwd + dg_lserk4_adj_ex
+ * sweep pair with src_coef = 0 (terminal functionals, e.g. J = |u^N|^2/2 with w = u^N).
+ *
+ * dg_lserk4_fwd_rec: uN = u^nsteps from u0 = u^0 (u0 untouched unless uN == u0).
+ *   jumps (device, 16-byte aligned, 2*nsteps*batch*K doubles): for n = 1..nsteps and element
+ *   e, jumps[2*((n-1)*batch*K + e) + {0, 1}] = {du0 - du1, du0 + du1} of u^n at t_n.
+ * dg_lserk4_adj_rec: dg_lserk4_adj_ex(w, snapshots, src_coef = 0, eta, flags) with the
+ *   record of the same sweep in place of the snapshots (jumps may be null if eta is). */
+int dg_lserk4_fwd_rec(dg_plan* plan, const double* u0, double* uN, double t0, double dt,
+                      int nsteps, double* jumps, void* stream);
+int dg_lserk4_adj_rec(dg_plan* plan, double* w, const double* jumps, double t0, double dt,
+                      int nsteps, double* eta, int flags, void* stream);
+
 /* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */
 int dg_slope_limit_n(dg_plan* plan, const double* u, double* ulim, int32_t* ids_mask,

@@ -1,0 +1,192 @@
+"""The snapshot-free sweep pair (dg_lserk4_fwd_rec / dg_lserk4_adj_rec, include/dg_advec.h).
+
+For linear advection the adjoint step S^T does not depend on the state and the indicator
+needs of each u^n only its two interelement jumps per element (R = LIFT*(Fscale.*du),
+utils/AdvecRHS1D.m:19).  The forward records (du0 - du1, du0 + du1) per element and step in
+place of the snapshots.  Bars:
+  * the record equals the jumps of the snapshot sweep's states, bit for bit (same doubles,
+    same subtractions), and agrees with the oracle's AdvecRHS1D face jumps (face_jumps,
+    which carry the (a nx)/2 factors) to rounding;
+  * final state, w^0 and eta equal the snapshot sweep pair's (src_coef = 0) bit for bit,
+    for every tile shape, steps per launch, batch (trajectory edges inside tiles), inflow
+    variant and a refined (non-uniform) mesh.
+"""
+import numpy as np
+import pytest
+
+from oracle import advec as oadv
+from oracle import setup1d
+
+pytestmark = pytest.mark.gpu
+
+
+def host(t):
+  return t.detach().cpu().numpy()
+
+
+def raw_jumps(u_em, K, batch, Np, uin):
+  """(du0 - du1, du0 + du1) per element of an element-major field: du0 = u_0 - (left
+  neighbour's u_N, or the inflow value), du1 = u_N - (right neighbour's u_0, or u_N)."""
+  u = u_em.reshape(batch, K, Np)
+  left = np.concatenate([np.full((batch, 1), uin), u[:, :-1, Np - 1]], axis=1)
+  right = np.concatenate([u[:, 1:, 0], u[:, -1:, Np - 1]], axis=1)
+  du0 = u[:, :, 0] - left
+  du1 = u[:, :, Np - 1] - right
+  return np.stack([du0 - du1, du0 + du1], axis=-1).reshape(batch * K, 2)
+
+
+def sweep_pair(pkg, op, u0, dt, nsteps, t0=0.0):
+  """The snapshot pair and the record pair from the same u0; returns both results."""
+  import torch
+  snaps = op.new_field(nsteps + 1)
+  snaps[0].copy_(u0)
+  op.forward(snaps[0], t0, dt, nsteps, snaps)
+  w_s = snaps[nsteps].clone()
+  eta_s = torch.zeros(op.ktot, dtype=torch.float64, device=op.device)
+  op.adjoint(w_s, snaps, t0, dt, nsteps, eta=eta_s)
+  rec = op.new_jumps(nsteps)
+  uN = op.new_field()
+  op.forward_rec(u0, t0, dt, nsteps, rec, out=uN)
+  w_r = uN.clone()
+  eta_r = torch.full((op.ktot,), float("nan"), dtype=torch.float64, device=op.device)
+  op.adjoint_rec(w_r, rec, t0, dt, nsteps, eta=eta_r, eta_assign=True)
+  torch.cuda.synchronize()
+  return snaps, w_s, eta_s, rec, uN, w_r, eta_r
+
+
+@pytest.mark.parametrize("N,K,batch,tw,spl,nsteps,inflow", [
+    (4, 1000, 1, 1, 4, 9, "a"),
+    (4, 700, 3, 1, 4, 8, "a2"),
+    (4, 600, 2, 2, 8, 17, "a"),
+    (3, 513, 1, 2, 4, 6, "a"),
+    (2, 900, 2, 1, 2, 5, "a2"),
+    (1, 300, 1, 1, 1, 3, "a"),
+    (6, 260, 1, 1, 4, 4, "a"),
+    (8, 400, 1, 2, 2, 7, "a"),
+    (4, 77, 1, 1, 4, 2, "a"),     # one launch, fewer steps than steps_per_launch
+])
+def test_record_pair_equals_snapshot_pair(pkg, gpu, N, K, batch, tw, spl, nsteps, inflow):
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
+  op.tune(tile_width=tw, steps_per_launch=spl, lane_elements=0)
+  dt = mesh.cfl_dt()
+  u0 = op.new_field()
+  rng = np.random.default_rng(N * 100 + K)
+  op.init_sine(rng.uniform(0.5, 1.5, batch), rng.integers(1, 5, batch).astype(float),
+               rng.uniform(0, 6, batch), out=u0)
+  u0_copy = u0.clone()
+  snaps, w_s, eta_s, rec, uN, w_r, eta_r = sweep_pair(pkg, op, u0, dt, nsteps, t0=0.01)
+  np.testing.assert_array_equal(host(u0), host(u0_copy))  # u0 untouched
+  np.testing.assert_array_equal(host(uN), host(snaps[nsteps]))
+  # the record: u^n's jumps at t_n, n = 1..nsteps
+  t = [0.01]
+  for _ in range(nsteps):
+    t.append(t[-1] + dt)
+  R = host(rec)
+  for n in range(1, nsteps + 1):
+    uin = oadv.inflow_value(op.a, t[n], inflow)
+    np.testing.assert_array_equal(R[n - 1], raw_jumps(host(snaps[n]), K, batch, N + 1, uin),
+                                  err_msg=f"record {n - 1}")
+  np.testing.assert_array_equal(host(w_r), host(w_s))
+  np.testing.assert_array_equal(host(eta_r), host(eta_s))
+  assert np.abs(host(eta_s)).max() > 0
+
+
+def test_record_is_the_oracle_face_jumps(pkg, gpu):
+  """The recorded raw jumps are AdvecRHS1D's du (utils/AdvecRHS1D.m:9-16, oracle face_jumps)
+  up to its (a nx)/2 factors: du_left = -(a/2) du0, du_right = (a/2) du1."""
+  N, K, nsteps = 4, 200, 4
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  S = setup1d.startup1d(N, np.linspace(0.0, 1.0, K + 1))
+  dt = mesh.cfl_dt()
+  u0 = op.new_field()
+  op.init_sine([1.0], [1.0], [0.0], out=u0)
+  snaps = op.new_field(nsteps + 1)
+  snaps[0].copy_(u0)
+  op.forward(snaps[0], 0.0, dt, nsteps, snaps)
+  rec = op.new_jumps(nsteps)
+  op.forward_rec(u0, 0.0, dt, nsteps, rec, out=op.new_field())
+  R = host(rec)
+  t = 0.0
+  for n in range(1, nsteps + 1):
+    t += dt
+    u = setup1d.from_elem_major(host(snaps[n]), N + 1)
+    du = oadv.face_jumps(u, oadv.inflow_value(op.a, t, "a"), op.a, S)
+    du0 = 0.5 * (R[n - 1, :, 0] + R[n - 1, :, 1])
+    du1 = 0.5 * (R[n - 1, :, 1] - R[n - 1, :, 0])
+    np.testing.assert_allclose(du[0], -0.5 * op.a * du0, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(du[1], 0.5 * op.a * du1, rtol=1e-12, atol=1e-12)
+
+
+def test_record_pair_on_a_refined_mesh(pkg, gpu):
+  """Non-uniform metric (the refine loop's meshes): still bit-identical to the snapshots."""
+  N, K, nsteps = 4, 500, 8
+  v_x = np.linspace(0.0, 1.0, K + 1)
+  for k in (3, 170, 171, 499):
+    v_x = np.insert(v_x, k + 1, 0.5 * (v_x[k] + v_x[k + 1]))
+  mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+  op = pkg.operators.DGAdvection1D(mesh, batch=2)
+  assert not op.uniform
+  dt = mesh.cfl_dt()
+  u0 = op.new_field()
+  op.init_sine([1.0, 0.7], [2.0, 3.0], [0.0, 1.0], out=u0)
+  snaps, w_s, eta_s, rec, uN, w_r, eta_r = sweep_pair(pkg, op, u0, dt, nsteps)
+  np.testing.assert_array_equal(host(uN), host(snaps[nsteps]))
+  np.testing.assert_array_equal(host(w_r), host(w_s))
+  np.testing.assert_array_equal(host(eta_r), host(eta_s))
+
+
+def test_record_in_place_and_flags(pkg, gpu):
+  """forward_rec in place on u0 (one launch and several), adjoint_rec's |eta| flag, the
+  empty sweep."""
+  import torch
+  N, K = 4, 300
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  dt = mesh.cfl_dt()
+  for nsteps in (1, 3, 10):
+    u0 = op.new_field()
+    op.init_sine([1.0], [1.0], [0.0], out=u0)
+    ref = op.new_field()
+    rec_a, rec_b = op.new_jumps(nsteps), op.new_jumps(nsteps)
+    op.forward_rec(u0, 0.0, dt, nsteps, rec_a, out=ref)
+    op.forward_rec(u0, 0.0, dt, nsteps, rec_b)  # in place
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(u0), host(ref))
+    np.testing.assert_array_equal(host(rec_a), host(rec_b))
+    w1, w2 = ref.clone(), ref.clone()
+    e1 = torch.zeros(K, dtype=torch.float64, device=gpu)
+    e2 = torch.zeros(K, dtype=torch.float64, device=gpu)
+    op.adjoint_rec(w1, rec_a, 0.0, dt, nsteps, eta=e1)
+    op.adjoint_rec(w2, rec_a, 0.0, dt, nsteps, eta=e2, eta_assign=True, eta_abs=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(w1), host(w2))
+    np.testing.assert_array_equal(np.abs(host(e1)), host(e2))
+  u0 = op.new_field()
+  op.init_sine([1.0], [1.0], [0.0], out=u0)
+  out = op.new_field()
+  op.forward_rec(u0, 0.0, dt, 0, op.new_jumps(0), out=out)
+  eta = torch.full((K,), 3.0, dtype=torch.float64, device=gpu)
+  op.adjoint_rec(out, op.new_jumps(0), 0.0, dt, 0, eta=eta, eta_assign=True)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(host(out), host(u0))
+  assert not host(eta).any()
+
+
+def test_record_rejects_what_it_cannot_do(pkg, gpu):
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=4, k=100)
+  op = pkg.operators.DGAdvection1D(mesh, flux="burgers", limiter=True)
+  u = op.new_field()
+  with pytest.raises(pkg._lib.DGLibraryError):
+    op.forward_rec(u, 0.0, 1e-4, 2, op.new_jumps(2))
+  lin = pkg.operators.DGAdvection1D(mesh)
+  u = lin.new_field()
+  lin.init_sine([1.0], [1.0], [0.0], out=u)
+  buf = torch.empty(2 * 2 * 100 + 1, dtype=torch.float64, device=gpu)
+  with pytest.raises(pkg._lib.DGLibraryError):  # 8-byte aligned only
+    lin.forward_rec(u, 0.0, 1e-4, 2, buf[1:])
+  with pytest.raises(ValueError):
+    lin.forward_rec(u, 0.0, 1e-4, 3, lin.new_jumps(2))
