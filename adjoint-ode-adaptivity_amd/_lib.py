@@ -19,6 +19,7 @@ DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T = 0, 1
 DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
 DG_TUNE_TILE_WIDTH, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
 DG_TUNE_LANE_ELEMENTS = 4
+DG_TUNE_REC_TILE_WIDTH, DG_TUNE_REC_STEPS_PER_LAUNCH = 5, 6
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
@@ -49,6 +50,7 @@ SIGNATURES = {
                                 ctypes.c_double, _vp, _i32, _vp, _vp]),
     "dg_lserk4_fwd_ex": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp,
                                 _vp]),
+    "dg_plan_query_rec": (_i32, [_vp, _vp]),
     "dg_lserk4_fwd_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,
                                  _vp]),
     "dg_lserk4_adj_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,

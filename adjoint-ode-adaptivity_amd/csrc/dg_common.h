@@ -436,6 +436,10 @@ struct dg_plan {
   // tuning (dg_plan_tune): tile width of the step kernels (tile = 256*tile_width elements)
   int tile_width = 1;  // dg_plan_create: 2 for N <= 2 (measured per-N)
   int msteps = 4;  // time steps fused per launch (1, 2 or 4)
+  // the jump-record sweeps' shape (dg_lserk4_fwd_rec / _adj_rec: no snapshot per step, so
+  // long launches on wide tiles pay): tile width 1, 2 or 4, steps per launch 1..8
+  int rec_tile_width = 2;
+  int rec_msteps = 8;
   int xcd_order = 1;  // XCD-aware tile order
   int lane_elems = 0;  // 0: workgroup tiles (one element per lane); 2 or 4: wave tiles
   // physics (dg_plan_set_physics): DG_FLUX_LINEAR / DG_FLUX_BURGERS, SlopeLimitN per stage

@@ -504,7 +504,10 @@ def main(argv=None):
   pkg.adaptive.check_indicator(ref_val, ref_idx)
 
   Np, ktot = N + 1, K * sweep.batch
-  ms = sweep.op.steps_per_launch
+  if args.record == "jumps":
+    ms, tw = sweep.op.rec_steps_per_launch, sweep.op.rec_tile_width
+  else:
+    ms, tw = sweep.op.steps_per_launch, sweep.op.tile_width
   chunks = sweep_chunks(nsteps, ms)
   launches = len(chunks)
   fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / launches for e in evs]
@@ -580,12 +583,12 @@ def main(argv=None):
                  "per_ic_gather": bool(args.gather_ics), "record": args.record},
       "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                   "kernel": f"k_adj<{Np},5,uniform,{sweep.op.tile_width},{ms}{rec_tag}> ({ms} reverse steps + DWR per launch)",
+                   "kernel": f"k_adj<{Np},5,uniform,{tw},{ms}{rec_tag}> ({ms} reverse steps + DWR per launch)",
                    "launch_us": adj_launch_us, "launch_us_stats": stats(adj_us),
                    "algorithmic_bytes": adj_bytes, "traffic_source": traffic_src},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_gbs / HBM_PEAK_GBS,
-                       "kernel": f"k_step<{Np},5,uniform,{sweep.op.tile_width},{ms}{rec_tag}> ({ms} steps per launch)",
+                       "kernel": f"k_step<{Np},5,uniform,{tw},{ms}{rec_tag}> ({ms} steps per launch)",
                        "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
       "step_ms_stats": stats(step_ms),
@@ -602,6 +605,7 @@ def main(argv=None):
                       "adj_frac_of_achievable": adj_gbs / copy_gbs if copy_gbs else None,
                       "fwd_frac_of_achievable": fwd_gbs / copy_gbs if copy_gbs else None},
       "steps_per_launch": ms,
+      "tile_width": tw,
       "launch_steps": chunks,
       "refine_index": ref_idx,
       "refine_value": ref_val,

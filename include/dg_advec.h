@@ -89,10 +89,18 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             on one-wave tiles of 64*value elements, value consecutive
  *                             elements per lane, cross-lane faces by DPP (LSERK4, Np <= 8;
  *                             bit-identical to the workgroup tiles at equal steps per launch)
- * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS. */
+ *   DG_TUNE_REC_TILE_WIDTH    1 or 2: tile width of the jump-record sweeps
+ *                             (dg_lserk4_fwd_rec / dg_lserk4_adj_rec; default 2)
+ *   DG_TUNE_REC_STEPS_PER_LAUNCH  1, 2, 4 or 8: their steps per launch (default 8; 8 needs
+ *                             tile width 2, else 4 is used; Np = 9 caps it at 2)
+ * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
+ * DG_REC_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
-       DG_TUNE_LANE_ELEMENTS = 4 };
+       DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
+
+/* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch. */
+int dg_plan_query_rec(const dg_plan* plan, int64_t out[2]);
 
 /* Physics of the plan's steppers.  Default: DG_FLUX_LINEAR + DG_LIMIT_NONE (AdvecRHS1D).
  *   DG_FLUX_LINEAR      f(u) = a*u                               utils/AdvecRHS1D.m:9-19

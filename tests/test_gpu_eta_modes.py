@@ -54,25 +54,32 @@ def test_eta_assign_with_zero_steps_zeroes(pkg, gpu):
   assert not host(eta).any()
 
 
-def test_ensemble_rows_are_per_ic_magnitudes(pkg, gpu):
+@pytest.mark.parametrize("record", ["jumps", "snapshots"])
+def test_ensemble_rows_are_per_ic_magnitudes(pkg, gpu, record):
   """EnsembleSweep rows = |signed eta| of each IC run alone (Main_width_ref.py:139), their
   rank partial = the IC-order sum of the magnitudes, and the refine index = argmax of the
-  oracle's ensemble_indicator of the signed rows."""
+  oracle's ensemble_indicator of the signed rows -- with either indicator record."""
   import torch
   K, ics, nsteps = 256, [1, 2, 5, 6], 8
   mesh = pkg.BaseGalerkin1D(n=4, k=K)
   dt = mesh.cfl_dt()
-  sweep = pkg.ensemble.EnsembleSweep(mesh, ics, nsteps, dt)
+  sweep = pkg.ensemble.EnsembleSweep(mesh, ics, nsteps, dt, record=record)
   partial = sweep.run().clone()
   rows = host(sweep.per_ic())
   signed = []
   for j in ics:
     op = pkg.operators.DGAdvection1D(mesh)
-    snaps = op.new_field(nsteps + 1)
-    op.init_sine(*pkg.ensemble.ic_params([j]), out=snaps[0])
-    op.forward(snaps[0], 0.0, dt, nsteps, snaps)
     eta = torch.zeros(K, dtype=torch.float64, device=gpu)
-    op.adjoint(snaps[nsteps], snaps, 0.0, dt, nsteps, eta=eta)
+    if record == "jumps":
+      u0, w, rec = op.new_field(), op.new_field(), op.new_jumps(nsteps)
+      op.init_sine(*pkg.ensemble.ic_params([j]), out=u0)
+      op.forward_rec(u0, 0.0, dt, nsteps, rec, out=w)
+      op.adjoint_rec(w, rec, 0.0, dt, nsteps, eta=eta)
+    else:
+      snaps = op.new_field(nsteps + 1)
+      op.init_sine(*pkg.ensemble.ic_params([j]), out=snaps[0])
+      op.forward(snaps[0], 0.0, dt, nsteps, snaps)
+      op.adjoint(snaps[nsteps], snaps, 0.0, dt, nsteps, eta=eta)
     torch.cuda.synchronize()
     signed.append(host(eta))
   signed = np.array(signed)

@@ -54,22 +54,28 @@ def sweep_pair(pkg, op, u0, dt, nsteps, t0=0.0):
   return snaps, w_s, eta_s, rec, uN, w_r, eta_r
 
 
-@pytest.mark.parametrize("N,K,batch,tw,spl,nsteps,inflow", [
-    (4, 1000, 1, 1, 4, 9, "a"),
-    (4, 700, 3, 1, 4, 8, "a2"),
-    (4, 600, 2, 2, 8, 17, "a"),
-    (3, 513, 1, 2, 4, 6, "a"),
-    (2, 900, 2, 1, 2, 5, "a2"),
-    (1, 300, 1, 1, 1, 3, "a"),
-    (6, 260, 1, 1, 4, 4, "a"),
-    (8, 400, 1, 2, 2, 7, "a"),
-    (4, 77, 1, 1, 4, 2, "a"),     # one launch, fewer steps than steps_per_launch
+@pytest.mark.parametrize("N,K,batch,tw,rtw,spl,nsteps,inflow", [
+    (4, 1000, 1, 1, 1, 4, 9, "a"),
+    (4, 700, 3, 1, 2, 4, 8, "a2"),
+    (4, 600, 2, 2, 2, 8, 17, "a"),
+    (4, 2600, 2, 2, 2, 8, 20, "a"),
+    (5, 1800, 1, 1, 2, 4, 9, "a"),
+    (3, 513, 1, 2, 2, 4, 6, "a"),
+    (2, 900, 2, 1, 1, 2, 5, "a2"),
+    (1, 300, 1, 1, 2, 1, 3, "a"),
+    (6, 260, 1, 1, 1, 4, 4, "a"),
+    (8, 400, 1, 2, 2, 2, 7, "a"),
+    (4, 77, 1, 1, 1, 4, 2, "a"),     # one launch, fewer steps than steps_per_launch
 ])
-def test_record_pair_equals_snapshot_pair(pkg, gpu, N, K, batch, tw, spl, nsteps, inflow):
+def test_record_pair_equals_snapshot_pair(pkg, gpu, N, K, batch, tw, rtw, spl, nsteps, inflow):
+  """At equal steps per launch (which sets where the state leaves even/odd coordinates);
+  tile widths never change the arithmetic."""
   import torch
   mesh = pkg.BaseGalerkin1D(n=N, k=K)
   op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
-  op.tune(tile_width=tw, steps_per_launch=spl, lane_elements=0)
+  op.tune(tile_width=tw, steps_per_launch=spl, lane_elements=0, rec_tile_width=rtw,
+          rec_steps_per_launch=spl)
+  assert op.rec_steps_per_launch == op.steps_per_launch
   dt = mesh.cfl_dt()
   u0 = op.new_field()
   rng = np.random.default_rng(N * 100 + K)
@@ -128,6 +134,7 @@ def test_record_pair_on_a_refined_mesh(pkg, gpu):
     v_x = np.insert(v_x, k + 1, 0.5 * (v_x[k] + v_x[k + 1]))
   mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
   op = pkg.operators.DGAdvection1D(mesh, batch=2)
+  op.tune(rec_tile_width=1, rec_steps_per_launch=op.steps_per_launch)
   assert not op.uniform
   dt = mesh.cfl_dt()
   u0 = op.new_field()
