@@ -45,7 +45,9 @@ if ROOT not in sys.path:
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec peak (AMD data sheet; not in the guide)
-PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+PROFILE_TRAFFIC = {  # per-launch PMC traffic of the sweep kernels (profiles/r02/collect.sh)
+    "jumps": os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
+    "snapshots": os.path.join(ROOT, "profiles", "r02", "pmc_traffic_snapshots.json")}
 
 
 def parse(argv=None):
@@ -534,9 +536,9 @@ def main(argv=None):
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
-  if os.path.exists(PROFILE_TRAFFIC):
+  if os.path.exists(PROFILE_TRAFFIC[args.record]):
     try:
-      with open(PROFILE_TRAFFIC) as f:
+      with open(PROFILE_TRAFFIC[args.record]) as f:
         tr = json.load(f)
       if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
           and tr.get("steps_per_launch") == ms
@@ -546,6 +548,18 @@ def main(argv=None):
     except (OSError, ValueError):
       pass
 
+  # Jump record: the same launches priced with the snapshot sweep's algorithmic bytes (what
+  # the snapshot algorithm moves for the same steps) -- an effective rate, not HBM traffic.
+  effective = None
+  if args.record == "jumps":
+    snap_fwd = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in chunks]))
+    snap_adj = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
+    eff_adj = snap_adj / (adj_launch_us * 1e-6) / 1e9
+    eff_fwd = snap_fwd / (fwd_launch_us * 1e-6) / 1e9
+    effective = {"what": "launch times priced with the snapshot sweep's algorithmic bytes for "
+                         "the same steps (effective, not moved)",
+                 "adj_GBs": eff_adj, "adj_frac": eff_adj / HBM_PEAK_GBS,
+                 "fwd_GBs": eff_fwd, "fwd_frac": eff_fwd / HBM_PEAK_GBS}
   total_dofs = sum_over_ranks(sweep.dof_updates, world, dev, args.backend) * args.steps
   value = total_dofs / elapsed
   # The single-step algorithm moves 16 B (fwd) + 24 B + 16/Np B (adj) per pair of
@@ -591,6 +605,7 @@ def main(argv=None):
                        "kernel": f"k_step<{Np},5,uniform,{tw},{ms}{rec_tag}> ({ms} steps per launch)",
                        "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
+      "roofline_effective": effective,
       "step_ms_stats": stats(step_ms),
       "single_step_roofline": {"value": single_step_roofline, "unit": "DOF-updates/s",
                                "bytes_per_update": single_step_bytes,

@@ -1,6 +1,6 @@
 """Minimal driver for counter collection on one step kernel (no timing, no checks):
 
-  python profiles/kernel_driver.py --what fwd_nosnap|fwd|adj [--N 4] [--K 1048576] [--reps 3]
+  python profiles/kernel_driver.py --what fwd_nosnap|fwd|adj|fwd_rec|adj_rec [--N 4] [--K 1048576] [--reps 3]
                                    [--physics linear|burgers_limited] [--nonuniform]
 
 Runs `reps` sweeps of --nsteps steps of the chosen kernel after one warm-up sweep.
@@ -52,8 +52,17 @@ def main():
   w = op.new_field()
   eta = torch.zeros(op.ktot, dtype=torch.float64, device=op.device)
   u = op.new_field()
+  jumps = None
+  if a.what.endswith("_rec"):  # the jump-record sweeps (their own default shape)
+    jumps = op.new_jumps(a.nsteps)
+    op.forward_rec(snaps[0], 0.0, dt, a.nsteps, jumps, out=u)
   for _ in range(a.reps + 1):
-    if a.what == "fwd_nosnap":
+    if a.what == "fwd_rec":
+      op.forward_rec(snaps[0], 0.0, dt, a.nsteps, jumps, out=u)
+    elif a.what == "adj_rec":
+      w.copy_(u)
+      op.adjoint_rec(w, jumps, 0.0, dt, a.nsteps, eta=eta)
+    elif a.what == "fwd_nosnap":
       u.copy_(snaps[0])
       op.forward(u, 0.0, dt, a.nsteps)
     elif a.what == "fwd":

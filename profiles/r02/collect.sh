@@ -14,4 +14,6 @@ STATS=$(find "$OUT/prof" -name '*kernel_stats.csv' -print -quit)
 FETCH=$(find "$OUT/pmc_fetch" -name '*counter_collection.csv' -print -quit)
 WRITE=$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)
 cp "$STATS" "$OUT/kernel_stats.csv"
-python3 profiles/summarize.py --stats "$STATS" --fetch "$FETCH" --write "$WRITE" --out "$OUT/summary.json" --traffic-json "$OUT/pmc_traffic.json" > /dev/null && echo collected
+REC=jumps; SPL=8
+case " $* " in *" --record snapshots "*) REC=snapshots; SPL=4;; esac
+python3 profiles/summarize.py --stats "$STATS" --fetch "$FETCH" --write "$WRITE" --out "$OUT/summary.json" --traffic-json "$OUT/pmc_traffic.json" --record $REC --steps-per-launch $SPL > /dev/null && echo collected

@@ -40,6 +40,7 @@ def main():
   p.add_argument("--K", type=int, default=1 << 20)
   p.add_argument("--steps-per-launch", type=int, default=4)
   p.add_argument("--batch", type=int, default=1)
+  p.add_argument("--record", default="jumps", choices=("jumps", "snapshots"))
   a = p.parse_args()
   out = collections.OrderedDict()
   for r in csv.DictReader(open(a.stats)):
@@ -53,6 +54,7 @@ def main():
       d = out.setdefault(k, {})
       d[cnt + "_KiB_avg"] = sum(v) / len(v)
       d[cnt.split("_")[0].lower() + "_bytes_corrected"] = scale * 1024.0 * sum(v) / len(v)
+      d[cnt.split("_")[0].lower() + "_dispatches"] = len(v)
   json.dump(out, open(a.out, "w"), indent=1)
   print(json.dumps(out, indent=1))
   if a.traffic_json:
@@ -61,15 +63,23 @@ def main():
       if "fetch_bytes_corrected" in d and "write_bytes_corrected" in d:
         return d["fetch_bytes_corrected"] + d["write_bytes_corrected"]
       return None
-    adj = [k for k in out if k.startswith("k_adj")]
-    fwd = [k for k in out if k.startswith("k_step")]
+    def sweep_mean(prefix):
+      # a sweep's launches may run several instantiations (e.g. 8 + 8 + 4 steps): the
+      # dispatch-weighted mean per launch over all of them, as bench.py averages its bytes
+      keys = [k for k in out if k.startswith(prefix) and hbm(k) is not None]
+      n = sum(out[k].get("fetch_dispatches", 0) for k in keys)
+      if not keys or n == 0:
+        return keys, None
+      return keys, sum(hbm(k) * out[k]["fetch_dispatches"] for k in keys) / n
+
+    adj, adj_b = sweep_mean("k_adj")
+    fwd, fwd_b = sweep_mean("k_step")
     tr = {"N": a.N, "K": a.K, "batch": a.batch, "steps_per_launch": a.steps_per_launch,
-          "source": a.out,
-          "adj_kernel": adj[0] if adj else None,
-          "adj_bytes_per_launch": hbm(adj[0]) if adj else None,
-          "fwd_kernel": fwd[0] if fwd else None,
-          "fwd_bytes_per_launch": hbm(fwd[0]) if fwd else None,
-          "note": "FETCH_SIZE x2 (gfx950 16-B/lane half count) + WRITE_SIZE, KiB->bytes"}
+          "record": a.record, "source": a.out,
+          "adj_kernel": adj, "adj_bytes_per_launch": adj_b,
+          "fwd_kernel": fwd, "fwd_bytes_per_launch": fwd_b,
+          "note": "FETCH_SIZE x2 (gfx950 16-B/lane half count) + WRITE_SIZE, KiB->bytes; "
+                  "dispatch-weighted mean over the sweep's kernel instantiations"}
     json.dump(tr, open(a.traffic_json, "w"), indent=1)
 
 
