@@ -422,7 +422,12 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 #pragma unroll
     for (int ss = 0; ss < NS; ++ss) {
       const int s = NS - 1 - ss;
-      const int f0 = G::kFB + (ss & 1) * 2 * (T + 2);  // g0 = lds[f0 ...], g1 = lds[f1 ...]
+      // Face buffers alternate over the launch's global reverse-stage index: with the jump
+      // record no barrier separates a step's last stage from the next step's first, so
+      // alternating on ss alone (NS = 5: 4 -> 0) would let a fast wave overwrite faces a
+      // slower neighbour wave has not read yet.
+      const int f0 = G::kFB + (((MS - 1 - st) * NS + ss) & 1) * 2 * (T + 2);
+      // g0 = lds[f0 ...], g1 = lds[f1 ...]
       const int f1 = f0 + (T + 2);
       double qe[EPL][NE], qo[EPL][NO];
       double g0[EPL], g1[EPL];
@@ -980,9 +985,23 @@ int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const 
 
 // Shapes: W = 1 with 1..4 steps, W = 2 with 1..8; Np = 9: at most 2 steps.  (1024-element
 // tiles -- 16-wave workgroups, 74 KB of LDS -- measured 20 % slower at N = 4, 8 steps.)
+inline bool rec_pairs(const dg_plan* p) { return p->rec_lane_elems == 2 && p->NP <= 8; }
+
+// Record steps per launch: pair tiles take 1, 2, 4, 5, 8, 10, 16 or 20 (a sweep is chunked by
+// halving: 20 -> 10 -> 5 -> 2 -> 1); the one-element-per-lane kernels 1, 2, 4 or 8.
+inline bool rec_msteps_ok(int k) {
+  return k == 1 || k == 2 || k == 4 || k == 5 || k == 8 || k == 10 || k == 16 || k == 20;
+}
+
 inline int rec_msteps(const dg_plan* p) {
   int m = p->rec_msteps;
-  if (m == 8 && p->rec_tile_width == 1) m = 4;
+  if (!rec_pairs(p)) {
+    int q = 1;
+    while (q * 2 <= m && q < 8) q *= 2;
+    m = q;
+  }
+  if (m == 8 && p->rec_tile_width == 1 && !rec_pairs(p)) m = 4;
+  if (rec_pairs(p) && p->rec_tile_width == 1 && m > 10) m = (m == 16) ? 8 : 10;
   if (p->NP > 8 && m > 2) m = 2;
   return m;
 }
@@ -994,6 +1013,8 @@ inline int rec_width(const dg_plan* p, int /*ms*/) { return p->rec_tile_width; }
 template <int NP>
 int launch_step_rec_t(const dg_plan* p, int ms, const double* in, double* rec, double* last,
                       const double* times, double dt, hipStream_t st, RecPos pos) {
+  if (rec_pairs(p))
+    return pair_launch_step_rec(p, ms, in, rec, last, times, dt, st, pos.n0, pos.jend);
   const int w = rec_width(p, ms);
   const bool w2 = w == 2;
   if constexpr (NP <= 8) {
@@ -1011,6 +1032,8 @@ template <int NP>
 int launch_adj_rec_t(const dg_plan* p, int ms, const double* win, double* wout, const double* rec,
                      double* eta, int em, const double* t_next, const double* src, double dt,
                      hipStream_t st, int64_t n0) {
+  if (rec_pairs(p))
+    return pair_launch_adj_rec(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
   const int w = rec_width(p, ms);
   const bool w2 = w == 2;
   if constexpr (NP <= 8) {
@@ -1131,6 +1154,9 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   // leave a 4-step launch in a 20-step sweep.)
   p->tile_width = (N <= 2) ? 2 : 1;
   if (N <= 2) p->lane_elems = 4;
+  // Record sweeps: pair tiles (2 elements per lane, 512-element tiles, dg_rec.hip) for
+  // Np <= 8; at Np = 9 the one-element-per-lane kernels on 512-element tiles, 2 steps.
+  if (p->NP > 8) p->rec_tile_width = 2;
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);
@@ -1150,7 +1176,11 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     }
     if (const char* v = std::getenv("DG_REC_STEPS_PER_LAUNCH")) {
       const int k = std::atoi(v);
-      if (k == 1 || k == 2 || k == 4 || k == 8) p->rec_msteps = k;
+      if (rec_msteps_ok(k)) p->rec_msteps = k;
+    }
+    if (const char* v = std::getenv("DG_REC_LANE_ELEMENTS")) {
+      const int k = std::atoi(v);
+      if (k == 1 || k == 2) p->rec_lane_elems = k;
     }
   }
   auto cleanup = [&](const std::string& m) {
@@ -1199,11 +1229,12 @@ int dg_plan_query(const dg_plan* p, int64_t out[8]) {
   return DG_OK;
 }
 
-int dg_plan_query_rec(const dg_plan* p, int64_t out[2]) {
+int dg_plan_query_rec(const dg_plan* p, int64_t out[3]) {
   if (!p || !out) return fail(DG_ERR_ARG, "null argument");
   const int m = rec_msteps(p);
   out[0] = rec_width(p, m);
   out[1] = m;
+  out[2] = rec_pairs(p) ? 2 : 1;
   return DG_OK;
 }
 
@@ -1216,9 +1247,14 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       p->rec_tile_width = int(value);
       return DG_OK;
     case DG_TUNE_REC_STEPS_PER_LAUNCH:
-      if (value != 1 && value != 2 && value != 4 && value != 8)
-        return fail(DG_ERR_ARG, "record steps per launch must be 1, 2, 4 or 8");
+      if (!rec_msteps_ok(int(value)))
+        return fail(DG_ERR_ARG, "record steps per launch must be 1, 2, 4, 5, 8, 10, 16 or 20");
       p->rec_msteps = int(value);
+      return DG_OK;
+    case DG_TUNE_REC_LANE_ELEMENTS:
+      if (value != 1 && value != 2)
+        return fail(DG_ERR_ARG, "record lane elements must be 1 or 2");
+      p->rec_lane_elems = int(value);
       return DG_OK;
     case DG_TUNE_TILE_WIDTH:
       if (value != 1 && value != 2) return fail(DG_ERR_ARG, "tile width must be 1 or 2");

@@ -438,8 +438,9 @@ struct dg_plan {
   int msteps = 4;  // time steps fused per launch (1, 2 or 4)
   // the jump-record sweeps' shape (dg_lserk4_fwd_rec / _adj_rec: no snapshot per step, so
   // long launches on wide tiles pay): tile width 1, 2 or 4, steps per launch 1..8
-  int rec_tile_width = 2;
+  int rec_tile_width = 1;  // pair tiles: 512 elements on 256 lanes
   int rec_msteps = 8;
+  int rec_lane_elems = 2;  // 2: the pair tiles of dg_rec.hip (Np <= 8), 1: dg_advec.hip k_step/k_adj
   int xcd_order = 1;  // XCD-aware tile order
   int lane_elems = 0;  // 0: workgroup tiles (one element per lane); 2 or 4: wave tiles
   // physics (dg_plan_set_physics): DG_FLUX_LINEAR / DG_FLUX_BURGERS, SlopeLimitN per stage
@@ -562,5 +563,12 @@ int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
 // plan->lane_elems; `times` as for the workgroup-tile launchers.
 int wave_launch_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
                      const double* times, double dt, hipStream_t st);
+
+// Jump-record sweep launches on pair tiles (dg_rec.hip), selected by plan->rec_lane_elems == 2.
+int pair_launch_step_rec(const dg_plan* p, int ms, const double* in, double* rec, double* last,
+                         const double* times, double dt, hipStream_t st, int64_t n0, bool jend);
+int pair_launch_adj_rec(const dg_plan* p, int ms, const double* win, double* wout,
+                        const double* rec, double* eta, int em, const double* t_next, double dt,
+                        hipStream_t st, int64_t n0);
 
 }  // namespace dgk

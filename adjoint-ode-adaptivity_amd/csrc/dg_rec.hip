@@ -1,0 +1,623 @@
+// dg_rec.hip — the jump-record sweep pair (dg_lserk4_fwd_rec / dg_lserk4_adj_rec) on
+// workgroup tiles with E consecutive elements per lane ("pair tiles", plan->rec_lane_elems).
+//
+// Same arithmetic per element as k_step / k_adj<..., REC = true> in dg_advec.hip (so the
+// results are bit-identical at equal steps per launch); what changes is the layout:
+//   - lane l owns tile elements E*l .. E*l+E-1.  The face between a lane's own elements is a
+//     register read; only the lane's outer two faces go through LDS, so a stage writes and
+//     reads half the LDS words per element and a barrier covers twice the elements;
+//   - the E independent element chains per lane give the fp64 pipe instruction-level
+//     parallelism between a stage's barrier and its update;
+//   - a 256*W-lane workgroup covers 256*W*E elements: the default (W = 1) puts a 512-element
+//     tile on 4 waves instead of 8, so each stage barrier waits for half as many waves;
+//   - the face arrays alias the staging image (one barrier after the image is read and one
+//     before it is rewritten, per launch): 20.8 KB of LDS per 512-element tile.
+// Measured (N = 4, K = 2^20, bench, A/B on one box): 5.86-5.98e11 DOF-updates/s against
+// 5.67-5.70e11 for the one-element-per-lane record kernels; 1024-element tiles (W = 2, 8-wave
+// workgroups, 3 per CU) 5.65-5.68e11 despite half the halo; 4 elements per lane 5.3e11;
+// raised wave priority on the post-barrier chain, an unrolled step loop, no scheduling pins:
+// all within noise.
+// Sources: AdvecRHS1D (utils/AdvecRHS1D.m:9-19), the LSERK4 loop (utils/One_code.mlx:106-140),
+// the indicator pattern (python/Main_finite_difference.py:54-94); DESIGN.md §5.
+#include "dg_common.h"
+
+namespace {
+using namespace dgk;
+
+template <int NP, int W, int E> struct RpGeo {
+  static constexpr int LB = kBlock * W;  // lanes per workgroup
+  static constexpr int T = E * LB;       // elements per tile (incl. halo)
+  static constexpr int kTileD = T * NP + 2;  // staging image (+2: 16-byte realignment)
+  static constexpr int kVec = (kTileD + 2 * LB - 1) / (2 * LB);  // double2 loads per lane
+  static constexpr int kFaceD = 4 * (LB + 2);  // 2 double-buffered lane-face arrays, padded
+  static constexpr int kLds = ((kTileD > kFaceD ? kTileD : kFaceD) + 1) & ~1;
+};
+
+// Coalesced 16-byte loads of the tile image [e0, e0 + T) (zeros outside [0, nd)), issued
+// together, then written to LDS.  Returns the image's offset (0 or 1 double).
+template <int NP, int W, int E, bool EDGE>
+__device__ __forceinline__ int rp_load(const double* __restrict__ g, int64_t e0, int64_t nd,
+                                       double* __restrict__ lds) {
+  using G = RpGeo<NP, W, E>;
+  const int64_t d0 = e0 * NP;
+  const int64_t base = d0 & ~int64_t(1);
+  const int off = int(d0 - base);
+  const int nvec = (G::T * NP + off + 1) >> 1;
+  const double2* __restrict__ g2 = reinterpret_cast<const double2*>(g);
+  double2 r[G::kVec];
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = int(threadIdx.x) + q * G::LB;
+    const int64_t gd = base + 2 * int64_t(v);
+    double2 val = make_double2(0.0, 0.0);
+    if (v < nvec) {
+      if (!EDGE || (gd >= 0 && gd + 1 < nd)) {
+        val = g2[gd >> 1];
+      } else {
+        if (gd >= 0 && gd < nd) val.x = g[gd];
+        if (gd + 1 >= 0 && gd + 1 < nd) val.y = g[gd + 1];
+      }
+    }
+    r[q] = val;
+  }
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = int(threadIdx.x) + q * G::LB;
+    if (v < nvec) *reinterpret_cast<double2*>(&lds[2 * v]) = r[q];
+  }
+  return off;
+}
+
+// The TE interior elements from registers to the image (nodal; `dual`: from the adjoint's
+// dual coordinates), then 16-byte stores.  Callers barrier before (face reads done).
+template <int NP, int W, int E, int H, bool EDGE>
+__device__ __forceinline__ void rp_store(double* __restrict__ g, int64_t o0, int64_t nd,
+                                         double* __restrict__ lds,
+                                         const double (*ev)[(NP + 1) / 2],
+                                         const double (*od)[NP / 2], bool dual) {
+  using G = RpGeo<NP, W, E>;
+  constexpr int T = G::T, TE = T - 2 * H;
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int m = 0; m < E; ++m) {
+    const int el = E * lane + m;
+    if (el >= H && el < T - H) {
+      double* o = lds + (el - H) * NP;
+      if (dual) {
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          o[k] = 0.5 * (ev[m][k] + od[m][k]);
+          o[N - k] = 0.5 * (ev[m][k] - od[m][k]);
+        }
+        if constexpr (NE > NO) o[NO] = ev[m][NO];
+      } else {
+        from_eo<NP>(ev[m], od[m], o);
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (EDGE) {
+    const int64_t rem = nd - o0;
+    store_run<G::LB>(g, o0, rem < int64_t(TE) * NP ? rem : int64_t(TE) * NP, lds);
+  } else {
+    store_full<TE * NP, G::LB>(g, o0, lds);
+  }
+}
+
+__device__ __forceinline__ double2* rp_slot(double* rec, int64_t n, int64_t ktot, int64_t e) {
+  return reinterpret_cast<double2*>(rec) + (n * ktot + e);  // = dg_advec.hip jump_slot
+}
+
+template <int NP, bool UNI, int W, int E, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_step_rp(const double* __restrict__ uin,
+                                                        double* __restrict__ rec,
+                                                        double* __restrict__ last,
+                                                        const double* __restrict__ scale,
+                                                        StepArgs<NP, 5, MS> args);
+
+// Forward: MS LSERK4 steps of the tile; records u^{n0}..u^{n0+MS-1}'s jumps (and u^{n0+MS}'s
+// when the launch ends the sweep), writes u^{n0+MS} to `last`.  See step_tile (dg_advec.hip).
+template <int NP, bool UNI, int W, int E, int MS, bool EDGE>
+__device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t tile,
+                                             const double* __restrict__ uin,
+                                             double* __restrict__ rec, double* __restrict__ last,
+                                             const double* __restrict__ scale,
+                                             const StepArgs<NP, 5, MS>& args) {
+  using G = RpGeo<NP, W, E>;
+  constexpr int NS = 5, T = G::T, LB = G::LB;
+  constexpr int H = MS * NS + 1;  // the stage cone + the final state's neighbours
+  constexpr int TE = T - 2 * H;
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
+  constexpr int CB = G::kLds;  // lds[CB + st*NS + s] = inflow value of that stage
+  constexpr int FB = LB + 2;   // one face array
+  const int lane = threadIdx.x;
+  const int64_t e0 = tile * TE - H;
+  const int64_t nd = args.ktot * NP;
+
+  const int off = rp_load<NP, W, E, EDGE>(uin, e0, nd, lds);
+  if constexpr (EDGE) {
+    using SArgs = StepArgs<NP, NS, MS>;  // lane-indexed kernarg read, see step_tile
+    const double* ka = reinterpret_cast<const double*>(
+        kernarg_tail<decltype(&k_step_rp<NP, UNI, W, E, MS>), SArgs>() + offsetof(SArgs, uin));
+    if (lane <= MS * NS) lds[CB + lane] = ka[lane];
+  }
+  __syncthreads();
+  double ev[E][NE], od[E][NO];
+  Elem El[E];
+  double sc[E];
+#pragma unroll
+  for (int m = 0; m < E; ++m) {
+    const int el = E * lane + m;
+    const double* us = lds + off + el * NP;
+    to_eo<NP>(us, ev[m], od[m]);
+    El[m] = elem_info<H, T, EDGE>(e0, el, args.ktot, args.K);
+    sc[m] = args.sc;
+    if constexpr (!UNI) sc[m] *= El[m].inrange ? scale[El[m].kl] : 0.0;
+    // u^{n0}'s jumps (record n0-1) from the staged nodal values, as step_tile
+    if (args.n0 >= 1 && El[m].valid) {
+      const double uL = (EDGE && El[m].first) ? lds[CB] : us[-1];
+      const double uR = (EDGE && El[m].last) ? us[NP - 1] : us[NP];
+      const double du0 = us[0] - uL, du1 = us[NP - 1] - uR;
+      *rp_slot(rec, args.n0 - 1, args.ktot, El[m].e) = double2{du0 - du1, du0 + du1};
+    }
+  }
+  __syncthreads();  // the image is read: the face arrays alias it
+
+  double re[E][NE], ro[E][NO];
+  // The step loop stays rolled (8x less code than unrolled, measured equal or faster); the
+  // stage loop inside is unrolled, so the RK coefficients are immediates.
+#pragma unroll 1
+  for (int st = 0; st < MS; ++st) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int fL = ((st * NS + s) & 1) * 2 * FB;  // buffers alternate over the global stage
+      const int fR = fL + FB;
+      double u0[E], uN[E];
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+        u0[m] = ev[m][0] + od[m][0];
+        uN[m] = ev[m][0] - od[m][0];
+      }
+      lds[fL + lane + 1] = u0[0];      // the lane's left face
+      lds[fR + lane + 1] = uN[E - 1];  // the lane's right face
+      __builtin_amdgcn_sched_barrier(0);
+      double pe[E][NE], po[E][NO];
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          double t = (UNI && s > 0) ? RK<NS>::A(s) * re[m][k] : args.op.Qeo[k * NO] * od[m][0];
+#pragma unroll
+          for (int j = (UNI && s > 0) ? 0 : 1; j < NO; ++j)
+            t = fma(args.op.Qeo[k * NO + j], od[m][j], t);
+          pe[m][k] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          double t = (UNI && s > 0) ? RK<NS>::A(s) * ro[m][k] : args.op.Qoe[k * NE] * ev[m][0];
+#pragma unroll
+          for (int j = (UNI && s > 0) ? 0 : 1; j < NE; ++j)
+            t = fma(args.op.Qoe[k * NE + j], ev[m][j], t);
+          po[m][k] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pin(pe[m][k]);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) pin(po[m][k]);
+      }
+      __syncthreads();
+      // lane-1's right face / lane+1's left face (the pads feed halo elements only)
+      const double fromL = lds[fR + lane], fromR = lds[fL + lane + 2];
+      double uin_s = 0.0;
+      if constexpr (EDGE) uin_s = lds[CB + st * NS + s];
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+        double uL = (m == 0) ? fromL : uN[m - 1];
+        double uR = (m == E - 1) ? fromR : u0[m + 1];
+        if constexpr (EDGE) {
+          uL = El[m].first ? uin_s : uL;
+          uR = El[m].last ? uN[m] : uR;
+        }
+        const double dlt = uR - uL, sig = -(uL + uR);
+        if (s == 0 && st >= 1 && El[m].valid) {  // u^{n0+st}'s jumps (record n0+st-1)
+          const double du0 = u0[m] - uL, du1 = uN[m] - uR;
+          *rp_slot(rec, args.n0 + st - 1, args.ktot, El[m].e) = double2{du0 - du1, du0 + du1};
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          if constexpr (UNI) {
+            re[m][k] = fma(args.op.le[k], dlt, pe[m][k]);
+          } else {
+            const double a = sc[m] * fma(args.op.le[k], dlt, pe[m][k]);
+            re[m][k] = (s == 0) ? a : fma(RK<NS>::A(s), re[m][k], a);
+          }
+          ev[m][k] = fma(RK<NS>::B(s), re[m][k], ev[m][k]);
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          if constexpr (UNI) {
+            ro[m][k] = fma(args.op.lo[k], sig, po[m][k]);
+          } else {
+            const double a = sc[m] * fma(args.op.lo[k], sig, po[m][k]);
+            ro[m][k] = (s == 0) ? a : fma(RK<NS>::A(s), ro[m][k], a);
+          }
+          od[m][k] = fma(RK<NS>::B(s), ro[m][k], od[m][k]);
+        }
+      }
+    }
+  }
+  if (args.jend) {
+    // the sweep's final state u^{n0+MS}: one more face exchange for its jumps (record
+    // n0+MS-1), inflow at t_{n0+MS}
+    const int fL = ((MS * NS) & 1) * 2 * FB, fR = fL + FB;
+    double u0[E], uN[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+      u0[m] = ev[m][0] + od[m][0];
+      uN[m] = ev[m][0] - od[m][0];
+    }
+    lds[fL + lane + 1] = u0[0];
+    lds[fR + lane + 1] = uN[E - 1];
+    __syncthreads();
+    const double fromL = lds[fR + lane], fromR = lds[fL + lane + 2];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+      double uL = (m == 0) ? fromL : uN[m - 1];
+      double uR = (m == E - 1) ? fromR : u0[m + 1];
+      if constexpr (EDGE) {
+        uL = El[m].first ? lds[CB + MS * NS] : uL;
+        uR = El[m].last ? uN[m] : uR;
+      }
+      if (El[m].valid) {
+        const double du0 = u0[m] - uL, du1 = uN[m] - uR;
+        *rp_slot(rec, args.n0 + MS - 1, args.ktot, El[m].e) = double2{du0 - du1, du0 + du1};
+      }
+    }
+  }
+  __syncthreads();  // the last face reads are done: the image is rewritten
+  rp_store<NP, W, E, H, EDGE>(last, tile * TE * NP, nd, lds, ev, od, false);
+}
+
+template <int NP, bool UNI, int W, int E, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_step_rp(const double* __restrict__ uin,
+                                                        double* __restrict__ rec,
+                                                        double* __restrict__ last,
+                                                        const double* __restrict__ scale,
+                                                        StepArgs<NP, 5, MS> args) {
+  using G = RpGeo<NP, W, E>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  constexpr int H = MS * 5 + 1;
+  const int64_t e0 = tile * (G::T - 2 * H) - H;
+  if (edge_tile(e0, G::T, args.ktot, args.K))
+    rp_step_tile<NP, UNI, W, E, MS, true>(lds, tile, uin, rec, last, scale, args);
+  else
+    rp_step_tile<NP, UNI, W, E, MS, false>(lds, tile, uin, rec, last, scale, args);
+}
+
+// Adjoint: MS reverse steps st = MS-1..0 of the tile, each
+//   eta += DWR(u^{n0+st+1}'s recorded jumps, w^{n0+st+1});  w^{n0+st} = S^T w^{n0+st+1}
+// (terminal functionals only: no source).  See adj_tile (dg_advec.hip).
+template <int NP, bool UNI, int W, int E, int MS, bool EDGE>
+__device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t tile,
+                                            const double* __restrict__ win,
+                                            double* __restrict__ wout,
+                                            const double* __restrict__ rec,
+                                            double* __restrict__ eta,
+                                            const double* __restrict__ scale,
+                                            const AdjArgs<NP, MS>& args) {
+  using G = RpGeo<NP, W, E>;
+  constexpr int NS = 5, T = G::T, LB = G::LB;
+  constexpr int H = MS * NS;
+  constexpr int TE = T - 2 * H;
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
+  constexpr int FB = LB + 2;
+  const int lane = threadIdx.x;
+  const int64_t e0 = tile * TE - H;
+  const int64_t nd = args.ktot * NP;
+
+  const int off = rp_load<NP, W, E, EDGE>(win, e0, nd, lds);
+  // the jumps of u^{n0+st+1} (record n0+st): one 16-byte load per element and step,
+  // prefetched a step ahead
+  double2 jn[E];
+  bool jin[E];
+#pragma unroll
+  for (int m = 0; m < E; ++m) {
+    const int64_t e = e0 + E * lane + m;
+    jin[m] = e >= 0 && e < args.ktot;
+    jn[m] = jin[m] ? *rp_slot(const_cast<double*>(rec), args.n0 + MS - 1, args.ktot, e)
+                   : double2{0.0, 0.0};
+  }
+  __syncthreads();
+  double we[E][NE], wo[E][NO];
+  Elem El[E];
+  double sc[E], eacc[E];
+#pragma unroll
+  for (int m = 0; m < E; ++m) {
+    const int el = E * lane + m;
+    const double* w = lds + off + el * NP;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      we[m][k] = w[k] + w[N - k];
+      wo[m][k] = w[k] - w[N - k];
+    }
+    if constexpr (NE > NO) we[m][NO] = w[NO];
+    El[m] = elem_info<H, T, EDGE>(e0, el, args.ktot, args.K);
+    sc[m] = args.sc;
+    if constexpr (!UNI) sc[m] *= El[m].inrange ? scale[El[m].kl] : 0.0;
+    eacc[m] = 0.0;
+  }
+  __syncthreads();  // the image is read: the face arrays alias it
+
+#pragma unroll 1
+  for (int st = MS - 1; st >= 0; --st) {
+    double2 jc[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+      jc[m] = jn[m];
+      if (st > 0 && jin[m])
+        jn[m] = *rp_slot(const_cast<double*>(rec), args.n0 + st - 1, args.ktot,
+                         e0 + E * lane + m);
+    }
+    if (args.has_eta) {
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+        double pe = 0.0, po = 0.0;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[m][k], pe);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[m][k], po);
+        double c = fma(jc[m].x, pe, jc[m].y * po);
+        if constexpr (!UNI) c *= sc[m];
+        eacc[m] += c;
+      }
+    }
+    double le_[E][NE], lo_[E][NO];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+#pragma unroll
+      for (int k = 0; k < NE; ++k) le_[m][k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < NO; ++k) lo_[m][k] = 0.0;
+    }
+#pragma unroll
+    for (int ss = 0; ss < NS; ++ss) {
+      const int s = NS - 1 - ss;
+      // buffers alternate over the launch's global reverse-stage index (no barrier between
+      // a step's last stage and the next step's first)
+      const int f0 = (((MS - 1 - st) * NS + ss) & 1) * 2 * FB, f1 = f0 + FB;
+      double g0[E], g1[E], qe[E][NE], qo[E][NO];
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+        double gd = 0.0, gs = 0.0;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          le_[m][k] = fma(RK<NS>::B(s), we[m][k], le_[m][k]);
+          qe[m][k] = UNI ? le_[m][k] : sc[m] * le_[m][k];
+          gd = fma(args.op.le[k], qe[m][k], gd);
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          lo_[m][k] = fma(RK<NS>::B(s), wo[m][k], lo_[m][k]);
+          qo[m][k] = UNI ? lo_[m][k] : sc[m] * lo_[m][k];
+          gs = fma(args.op.lo[k], qo[m][k], gs);
+        }
+        g0[m] = gd + gs;
+        g1[m] = gs - gd;
+      }
+      lds[f0 + lane + 1] = g0[0];      // the lane's first element: adjoint of its uL
+      lds[f1 + lane + 1] = g1[E - 1];  // the lane's last element: adjoint of its uR
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+        // the transposed volume term and the carry need no neighbour data
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+          double t = we[m][j];
+#pragma unroll
+          for (int k = 0; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[m][k], t);
+          we[m][j] = t;
+        }
+#pragma unroll
+        for (int j = 0; j < NO; ++j) {
+          double t = wo[m][j];
+#pragma unroll
+          for (int k = 0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[m][k], t);
+          wo[m][j] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) le_[m][k] = RK<NS>::A(s) * le_[m][k];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) lo_[m][k] = RK<NS>::A(s) * lo_[m][k];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pin(we[m][k]);
+#pragma unroll
+        for (int k = 0; k < NO; ++k) pin(wo[m][k]);
+      }
+      __syncthreads();
+      // lane-1's last element's g1 / lane+1's first element's g0
+      const double fromL = lds[f1 + lane], fromR = lds[f0 + lane + 2];
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+        // edge tiles: nothing arrives at a trajectory's first element from the left (uL is
+        // the inflow); its last element's uR is its own u_N (du1 = 0)
+        double gl = (m == 0) ? fromL : g1[m - 1];
+        double gr = (m == E - 1) ? fromR : g0[m + 1];
+        if constexpr (EDGE) {
+          gl = El[m].first ? 0.0 : gl;
+          gr = El[m].last ? g1[m] : gr;
+        }
+        we[m][0] -= gl + gr;
+        wo[m][0] += gr - gl;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < E; ++m)
+    if (args.has_eta && El[m].valid) eta_update(eta, El[m].e, eacc[m], args.has_eta);
+  __syncthreads();  // the last face reads are done: the image is rewritten
+  rp_store<NP, W, E, H, EDGE>(wout, tile * TE * NP, nd, lds, we, wo, true);
+}
+
+template <int NP, bool UNI, int W, int E, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_adj_rp(const double* __restrict__ win,
+                                                       double* __restrict__ wout,
+                                                       const double* __restrict__ rec,
+                                                       double* __restrict__ eta,
+                                                       const double* __restrict__ scale,
+                                                       AdjArgs<NP, MS> args) {
+  using G = RpGeo<NP, W, E>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  constexpr int H = MS * 5;
+  const int64_t e0 = tile * (G::T - 2 * H) - H;
+  if (edge_tile(e0, G::T, args.ktot, args.K))
+    rp_adj_tile<NP, UNI, W, E, MS, true>(lds, tile, win, wout, rec, eta, scale, args);
+  else
+    rp_adj_tile<NP, UNI, W, E, MS, false>(lds, tile, win, wout, rec, eta, scale, args);
+}
+
+template <int NP, int W, int E, int MS>
+int rp_step_e(const dg_plan* p, const double* in, double* rec, double* last, const double* times,
+              double dt, hipStream_t st, int64_t n0, bool jend) {
+  StepArgs<NP, 5, MS> a;
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
+  a.sc = dt;
+  for (int m = 0; m < MS; ++m)
+    for (int s = 0; s < 5; ++s) a.uin[m * 5 + s] = inflow_value(p, times[m] + RK<5>::C(s) * dt);
+  a.uin[MS * 5] = inflow_value(p, times[MS]);
+  a.ktot = p->ktot;
+  a.stride = p->ktot * NP;
+  a.n0 = n0;
+  a.K = int32_t(p->K);
+  a.xcd = p->xcd_order;
+  a.jend = jend ? 1 : 0;
+  constexpr int TE = RpGeo<NP, W, E>::T - 2 * (MS * 5 + 1);
+  const unsigned grid = grid_for(p->ktot, TE);
+  if (p->uniform)
+    hipLaunchKernelGGL((k_step_rp<NP, true, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
+                       rec, last, p->d_scale, a);
+  else
+    hipLaunchKernelGGL((k_step_rp<NP, false, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
+                       rec, last, p->d_scale, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+template <int NP, int W, int E, int MS>
+int rp_adj_e(const dg_plan* p, const double* win, double* wout, const double* rec, double* eta,
+             int eta_mode, const double* t_next, double dt, hipStream_t st, int64_t n0) {
+  AdjArgs<NP, MS> a;
+  make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
+  a.sc = dt;
+  for (int m = 0; m < MS; ++m) {
+    a.uin_res[m] = inflow_value(p, t_next[m]);
+    a.src[m] = 0.0;
+  }
+  a.ktot = p->ktot;
+  a.stride = p->ktot * NP;
+  a.n0 = n0;
+  a.K = int32_t(p->K);
+  a.has_eta = eta != nullptr ? (eta_mode | kEtaOn) : 0;
+  a.xcd = p->xcd_order;
+  constexpr int TE = RpGeo<NP, W, E>::T - 2 * MS * 5;
+  const unsigned grid = grid_for(p->ktot, TE);
+  if (p->uniform)
+    hipLaunchKernelGGL((k_adj_rp<NP, true, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+                       wout, rec, eta, p->d_scale, a);
+  else
+    hipLaunchKernelGGL((k_adj_rp<NP, false, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+                       wout, rec, eta, p->d_scale, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+// Shapes: 2 elements per lane, tile width 1 or 2 (512 or 1024 elements per tile), 1, 2, 4, 5,
+// 8, 10, 16 or 20 steps per launch (16 and 20 only at width 2: the cone leaves too few output
+// elements of a 512-element tile); Np <= 8.
+template <int NP, int W>
+int rp_step_w(const dg_plan* p, int ms, const double* in, double* rec, double* last,
+              const double* times, double dt, hipStream_t st, int64_t n0, bool jend) {
+  switch (ms) {
+    case 20: if constexpr (W == 2) return rp_step_e<NP, W, 2, 20>(p, in, rec, last, times, dt, st, n0, jend); break;
+    case 16: if constexpr (W == 2) return rp_step_e<NP, W, 2, 16>(p, in, rec, last, times, dt, st, n0, jend); break;
+    case 10: return rp_step_e<NP, W, 2, 10>(p, in, rec, last, times, dt, st, n0, jend);
+    case 8: return rp_step_e<NP, W, 2, 8>(p, in, rec, last, times, dt, st, n0, jend);
+    case 5: return rp_step_e<NP, W, 2, 5>(p, in, rec, last, times, dt, st, n0, jend);
+    case 4: return rp_step_e<NP, W, 2, 4>(p, in, rec, last, times, dt, st, n0, jend);
+    case 2: return rp_step_e<NP, W, 2, 2>(p, in, rec, last, times, dt, st, n0, jend);
+    case 1: return rp_step_e<NP, W, 2, 1>(p, in, rec, last, times, dt, st, n0, jend);
+    default: break;
+  }
+  return fail(DG_ERR_ARG, "pair tiles: unsupported steps per launch for this tile width");
+}
+
+template <int NP, int W>
+int rp_adj_w(const dg_plan* p, int ms, const double* win, double* wout, const double* rec,
+             double* eta, int em, const double* t_next, double dt, hipStream_t st, int64_t n0) {
+  switch (ms) {
+    case 20: if constexpr (W == 2) return rp_adj_e<NP, W, 2, 20>(p, win, wout, rec, eta, em, t_next, dt, st, n0); break;
+    case 16: if constexpr (W == 2) return rp_adj_e<NP, W, 2, 16>(p, win, wout, rec, eta, em, t_next, dt, st, n0); break;
+    case 10: return rp_adj_e<NP, W, 2, 10>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 8: return rp_adj_e<NP, W, 2, 8>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 5: return rp_adj_e<NP, W, 2, 5>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 4: return rp_adj_e<NP, W, 2, 4>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 2: return rp_adj_e<NP, W, 2, 2>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 1: return rp_adj_e<NP, W, 2, 1>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    default: break;
+  }
+  return fail(DG_ERR_ARG, "pair tiles: unsupported steps per launch for this tile width");
+}
+
+template <int NP>
+int rp_step_np(const dg_plan* p, int ms, const double* in, double* rec, double* last,
+               const double* times, double dt, hipStream_t st, int64_t n0, bool jend) {
+  if (p->rec_tile_width == 2) return rp_step_w<NP, 2>(p, ms, in, rec, last, times, dt, st, n0, jend);
+  return rp_step_w<NP, 1>(p, ms, in, rec, last, times, dt, st, n0, jend);
+}
+
+template <int NP>
+int rp_adj_np(const dg_plan* p, int ms, const double* win, double* wout, const double* rec,
+              double* eta, int em, const double* t_next, double dt, hipStream_t st, int64_t n0) {
+  if (p->rec_tile_width == 2)
+    return rp_adj_w<NP, 2>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+  return rp_adj_w<NP, 1>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+}
+
+}  // namespace
+
+namespace dgk {
+
+int pair_launch_step_rec(const dg_plan* p, int ms, const double* in, double* rec, double* last,
+                         const double* times, double dt, hipStream_t st, int64_t n0, bool jend) {
+  switch (p->NP) {
+    case 2: return rp_step_np<2>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    case 3: return rp_step_np<3>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    case 4: return rp_step_np<4>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    case 5: return rp_step_np<5>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    case 6: return rp_step_np<6>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    case 7: return rp_step_np<7>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    case 8: return rp_step_np<8>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    default: return fail(DG_ERR_ARG, "pair tiles support Np <= 8");
+  }
+}
+
+int pair_launch_adj_rec(const dg_plan* p, int ms, const double* win, double* wout,
+                        const double* rec, double* eta, int em, const double* t_next, double dt,
+                        hipStream_t st, int64_t n0) {
+  switch (p->NP) {
+    case 2: return rp_adj_np<2>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 3: return rp_adj_np<3>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 4: return rp_adj_np<4>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 5: return rp_adj_np<5>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 6: return rp_adj_np<6>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 7: return rp_adj_np<7>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 8: return rp_adj_np<8>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    default: return fail(DG_ERR_ARG, "pair tiles support Np <= 8");
+  }
+}
+
+}  // namespace dgk

@@ -45,6 +45,19 @@ if ROOT not in sys.path:
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec peak (AMD data sheet; not in the guide)
+# fp64 FMA probe on the box (profiles/probes/fp64_peak.hip, 8 waves/SIMD x 8 chains): the clock
+# gives back ~18 % under a dense fp64 load
+FP64_PROBE_TFLOPS = 64.6
+
+
+def eo_flops_per_update(Np, adjoint):
+  """fp64 flops per DOF-update that the even/odd kernels execute for an interior element
+  (per element-stage 4 + 5 Np + 4 NE NO forward; 6 + 5 Np + 4 NE NO reverse, plus
+  the indicator's 2 Np + 2 per element-step), counted like the bytes: the algorithm, no halo."""
+  NE, NO = (Np + 1) // 2, Np // 2
+  if not adjoint:
+    return 5.0 * (4 + 5 * Np + 4 * NE * NO) / Np
+  return (5.0 * (6 + 5 * Np + 4 * NE * NO) + 2 * Np + 2) / Np
 PROFILE_TRAFFIC = {  # per-launch PMC traffic of the sweep kernels (profiles/r02/collect.sh)
     "jumps": os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
     "snapshots": os.path.join(ROOT, "profiles", "r02", "pmc_traffic_snapshots.json")}
@@ -533,6 +546,9 @@ def main(argv=None):
     fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in chunks]))
     adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
   rec_tag = ",jumps" if args.record == "jumps" else ""
+  pairs = args.record == "jumps" and getattr(sweep.op, "rec_lane_elements", 1) == 2
+  kadj, kstep = ("k_adj_rp", "k_step_rp") if pairs else ("k_adj", "k_step")
+  tile_tag = f"{tw},2 elements/lane" if pairs else f"{tw}"
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
@@ -572,6 +588,9 @@ def main(argv=None):
   import torch.distributed as dist
   dist_world = dist.get_world_size() if dist.is_initialized() else 1
   idx_ranks = ranks_agree(ref_idx, world, dev, args.backend)
+  upl = Np * ktot * float(np.mean(chunks))  # DOF-updates per launch (sweep average)
+  adj_tf = eo_flops_per_update(Np, True) * upl / (adj_launch_us * 1e-6) / 1e12
+  fwd_tf = eo_flops_per_update(Np, False) * upl / (fwd_launch_us * 1e-6) / 1e12
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
       "value": value,
@@ -597,15 +616,24 @@ def main(argv=None):
                  "per_ic_gather": bool(args.gather_ics), "record": args.record},
       "roofline": {"bound": "hbm", "achieved": adj_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                   "kernel": f"k_adj<{Np},5,uniform,{tw},{ms}{rec_tag}> ({ms} reverse steps + DWR per launch)",
+                   "kernel": f"{kadj}<{Np},uniform,{tile_tag},{ms}{rec_tag}> ({ms} reverse steps + DWR per launch)",
                    "launch_us": adj_launch_us, "launch_us_stats": stats(adj_us),
                    "algorithmic_bytes": adj_bytes, "traffic_source": traffic_src},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_gbs / HBM_PEAK_GBS,
-                       "kernel": f"k_step<{Np},5,uniform,{tw},{ms}{rec_tag}> ({ms} steps per launch)",
+                       "kernel": f"{kstep}<{Np},uniform,{tile_tag},{ms}{rec_tag}> ({ms} steps per launch)",
                        "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
       "roofline_effective": effective,
+      # The compute roof of the same launches: the even/odd algorithm's fp64 flops (interior
+      # elements) / launch time, against the spec and the on-box FMA probe.
+      "roofline_fp64": {
+          "bound": "fp64 vector", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+          "probe_ceiling": FP64_PROBE_TFLOPS,
+          "adj_achieved": adj_tf, "adj_frac": adj_tf / FP64_PEAK_TFLOPS,
+          "fwd_achieved": fwd_tf, "fwd_frac": fwd_tf / FP64_PEAK_TFLOPS,
+          "flop_per_update": {"fwd": eo_flops_per_update(Np, False),
+                              "adj": eo_flops_per_update(Np, True)}},
       "step_ms_stats": stats(step_ms),
       "single_step_roofline": {"value": single_step_roofline, "unit": "DOF-updates/s",
                                "bytes_per_update": single_step_bytes,

@@ -197,3 +197,110 @@ def test_record_rejects_what_it_cannot_do(pkg, gpu):
     lin.forward_rec(u, 0.0, 1e-4, 2, buf[1:])
   with pytest.raises(ValueError):
     lin.forward_rec(u, 0.0, 1e-4, 3, lin.new_jumps(2))
+
+
+def rec_sweep(op, u0, dt, nsteps, t0=0.0):
+  """The record pair from u0 with the plan's current record shape."""
+  import torch
+  rec = op.new_jumps(nsteps)
+  uN = op.new_field()
+  op.forward_rec(u0, t0, dt, nsteps, rec, out=uN)
+  w = uN.clone()
+  eta = torch.full((op.ktot,), float("nan"), dtype=torch.float64, device=op.device)
+  op.adjoint_rec(w, rec, t0, dt, nsteps, eta=eta, eta_assign=True, eta_abs=True)
+  torch.cuda.synchronize()
+  return host(rec), host(uN), host(w), host(eta)
+
+
+@pytest.mark.parametrize("N,K,batch,rtw,spl,nsteps,inflow,refined", [
+    (4, 3000, 1, 2, 8, 20, "a", False),
+    (4, 2100, 3, 1, 8, 17, "a2", False),   # trajectory edges inside 512-element tiles
+    (4, 900, 2, 2, 4, 9, "a", True),
+    (4, 5000, 1, 1, 4, 6, "a", False),
+    (1, 1500, 2, 2, 8, 11, "a", False),
+    (2, 1100, 1, 1, 2, 5, "a2", True),
+    (3, 640, 2, 2, 8, 8, "a", False),
+    (5, 1030, 1, 2, 1, 3, "a", False),
+    (6, 700, 1, 1, 8, 16, "a", True),
+    (7, 800, 2, 2, 4, 4, "a", False),
+    (4, 50, 1, 2, 8, 3, "a", False),       # one edge tile holds the whole mesh
+])
+def test_pair_tiles_equal_one_element_per_lane(pkg, gpu, N, K, batch, rtw, spl, nsteps, inflow,
+                                               refined):
+  """The record sweeps on pair tiles (two consecutive elements per lane, dg_rec.hip) against
+  the one-element-per-lane record kernels at the same steps per launch: record, final state,
+  w^0 and |eta| bit for bit (tile shape never changes the arithmetic)."""
+  v_x = np.linspace(0.0, 1.0, K + 1)
+  if refined:
+    for k in (2, K // 3, K // 3 + 1, K - 1):
+      v_x = np.insert(v_x, k + 1, 0.5 * (v_x[k] + v_x[k + 1]))
+  mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+  op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
+  assert op.uniform != refined
+  dt = mesh.cfl_dt()
+  u0 = op.new_field()
+  rng = np.random.default_rng(N * 1000 + K)
+  op.init_sine(rng.uniform(0.5, 1.5, batch), rng.integers(1, 5, batch).astype(float),
+               rng.uniform(0, 6, batch), out=u0)
+  op.tune(rec_tile_width=2, rec_steps_per_launch=spl, rec_lane_elements=1)
+  assert (op.rec_steps_per_launch, op.rec_lane_elements) == (spl, 1)
+  ref = rec_sweep(op, u0, dt, nsteps, t0=0.02)
+  op.tune(rec_tile_width=rtw, rec_steps_per_launch=spl, rec_lane_elements=2)
+  assert (op.rec_tile_width, op.rec_steps_per_launch, op.rec_lane_elements) == (rtw, spl, 2)
+  got = rec_sweep(op, u0, dt, nsteps, t0=0.02)
+  for name, a, b in zip(("record", "u^N", "w^0", "|eta|"), got, ref):
+    np.testing.assert_array_equal(a, b, err_msg=name)
+  assert np.abs(ref[3]).max() > 0
+
+
+@pytest.mark.parametrize("N,K,batch,rtw,spl,nsteps", [
+    (4, 4000, 1, 1, 10, 20),   # 10 + 10
+    (4, 3000, 2, 2, 20, 20),   # one launch of 20 steps on 1024-element tiles
+    (4, 2500, 1, 2, 16, 23),   # 16 + 4 + 2 + 1
+    (1, 2000, 2, 1, 5, 17),    # 5 + 5 + 5 + 2
+    (7, 1500, 1, 2, 10, 13),   # 10 + 2 + 1
+    (4, 90, 1, 2, 20, 20),     # the whole mesh inside one edge tile
+])
+def test_pair_tiles_long_launches(pkg, gpu, N, K, batch, rtw, spl, nsteps):
+  """Pair tiles with 5, 10, 16 or 20 steps per launch (no one-element-per-lane counterpart):
+  against the snapshot sweep pair.  The states leave even/odd coordinates at other steps, so
+  u^N and w^0 agree to rounding (1e-12 relative), the record to 1e-12 of max|u|, and eta to
+  its conditioning (the jumps of a smooth solution are ~1e-7 of u: 1e-7 relative)."""
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh, batch=batch)
+  dt = mesh.cfl_dt()
+  u0 = op.new_field()
+  rng = np.random.default_rng(N * 7 + K)
+  op.init_sine(rng.uniform(0.5, 1.5, batch), rng.integers(1, 5, batch).astype(float),
+               rng.uniform(0, 6, batch), out=u0)
+  snaps, w_s, eta_s, _, _, _, _ = sweep_pair(pkg, op, u0, dt, nsteps)
+  op.tune(rec_tile_width=rtw, rec_steps_per_launch=spl, rec_lane_elements=2)
+  assert (op.rec_tile_width, op.rec_steps_per_launch, op.rec_lane_elements) == (rtw, spl, 2)
+  rec, uN, w, eta = rec_sweep(op, u0, dt, nsteps)
+  scale = np.abs(host(u0)).max()
+  np.testing.assert_allclose(uN, host(snaps[nsteps]), rtol=0, atol=1e-12 * scale)
+  np.testing.assert_allclose(w, host(w_s), rtol=0, atol=1e-12 * np.abs(host(w_s)).max())
+  for n in range(1, nsteps + 1):
+    uin = oadv.inflow_value(op.a, n * dt, "a")  # t_n by repeated addition: equal to rounding
+    ref = raw_jumps(host(snaps[n]), K, batch, N + 1, uin)
+    np.testing.assert_allclose(rec[n - 1], ref, rtol=0, atol=1e-12 * scale, err_msg=f"record {n - 1}")
+  e_ref = np.abs(host(eta_s))
+  np.testing.assert_allclose(eta, e_ref, rtol=0, atol=1e-7 * e_ref.max())
+
+
+def test_long_launch_shapes_are_checked(pkg, gpu):
+  """Width-1 pair tiles cap 16 / 20 steps at 8 / 10; the one-element-per-lane kernels take the
+  largest power of two <= the setting (<= 8); other values are refused."""
+  mesh = pkg.BaseGalerkin1D(n=4, k=500)
+  op = pkg.operators.DGAdvection1D(mesh)
+  op.tune(rec_tile_width=1, rec_lane_elements=2, rec_steps_per_launch=20)
+  assert op.rec_steps_per_launch == 10
+  op.tune(rec_steps_per_launch=16)
+  assert op.rec_steps_per_launch == 8
+  op.tune(rec_tile_width=2, rec_lane_elements=1, rec_steps_per_launch=10)
+  assert op.rec_steps_per_launch == 8
+  op.tune(rec_steps_per_launch=5)
+  assert op.rec_steps_per_launch == 4
+  for bad in (3, 6, 12, 32):
+    with pytest.raises(pkg._lib.DGLibraryError):
+      op.tune(rec_steps_per_launch=bad)
