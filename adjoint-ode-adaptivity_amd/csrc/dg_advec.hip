@@ -1154,9 +1154,8 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   // leave a 4-step launch in a 20-step sweep.)
   p->tile_width = (N <= 2) ? 2 : 1;
   if (N <= 2) p->lane_elems = 4;
-  // Record sweeps: pair tiles (2 elements per lane, 512-element tiles, dg_rec.hip) for
-  // Np <= 8; at Np = 9 the one-element-per-lane kernels on 512-element tiles, 2 steps.
-  if (p->NP > 8) p->rec_tile_width = 2;
+  // Record sweeps: pair tiles (2 elements per lane, dg_rec.hip) for Np <= 8; at Np = 9 the
+  // one-element-per-lane kernels on 512-element tiles, 2 steps (rec_msteps caps it).
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);

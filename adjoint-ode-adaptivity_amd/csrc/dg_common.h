@@ -438,8 +438,10 @@ struct dg_plan {
   int msteps = 4;  // time steps fused per launch (1, 2 or 4)
   // the jump-record sweeps' shape (dg_lserk4_fwd_rec / _adj_rec: no snapshot per step, so
   // long launches on wide tiles pay): tile width 1, 2 or 4, steps per launch 1..8
-  int rec_tile_width = 1;  // pair tiles: 512 elements on 256 lanes
-  int rec_msteps = 8;
+  // defaults measured at N = 4, K = 2^20: 1024-element pair tiles, 10 steps per
+  // launch (a 20-step sweep is 10 + 10 launches)
+  int rec_tile_width = 2;
+  int rec_msteps = 10;
   int rec_lane_elems = 2;  // 2: the pair tiles of dg_rec.hip (Np <= 8), 1: dg_advec.hip k_step/k_adj
   int xcd_order = 1;  // XCD-aware tile order
   int lane_elems = 0;  // 0: workgroup tiles (one element per lane); 2 or 4: wave tiles

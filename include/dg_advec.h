@@ -91,8 +91,8 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             bit-identical to the workgroup tiles at equal steps per launch)
  *   DG_TUNE_REC_TILE_WIDTH    1 or 2: tile width of the jump-record sweeps
  *                             (dg_lserk4_fwd_rec / dg_lserk4_adj_rec): workgroups of 256*value
- *                             lanes (default 1; 2 at Np = 9)
- *   DG_TUNE_REC_STEPS_PER_LAUNCH  their steps per launch (default 8): 1, 2, 4, 5, 8, 10, 16
+ *                             lanes (default 2)
+ *   DG_TUNE_REC_STEPS_PER_LAUNCH  their steps per launch (default 10): 1, 2, 4, 5, 8, 10, 16
  *                             or 20 on pair tiles (16 and 20 need tile width 2, else 8 / 10
  *                             are used), a sweep chunked by halving (20 -> 10 -> 5 -> 2 -> 1);
  *                             1, 2, 4 or 8 on one element per lane (8 needs tile width 2,

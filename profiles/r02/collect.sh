@@ -14,6 +14,8 @@ STATS=$(find "$OUT/prof" -name '*kernel_stats.csv' -print -quit)
 FETCH=$(find "$OUT/pmc_fetch" -name '*counter_collection.csv' -print -quit)
 WRITE=$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)
 cp "$STATS" "$OUT/kernel_stats.csv"
-REC=jumps; SPL=8
-case " $* " in *" --record snapshots "*) REC=snapshots; SPL=4;; esac
+REC=jumps
+case " $* " in *" --record snapshots "*) REC=snapshots;; esac
+# the bench line under rocprof names the sweep's steps per launch
+SPL=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['steps_per_launch'])" "$OUT/bench_under_rocprof.json")
 python3 profiles/summarize.py --stats "$STATS" --fetch "$FETCH" --write "$WRITE" --out "$OUT/summary.json" --traffic-json "$OUT/pmc_traffic.json" --record $REC --steps-per-launch $SPL > /dev/null && echo collected
