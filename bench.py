@@ -618,7 +618,12 @@ def main(argv=None):
                    "frac": adj_gbs / HBM_PEAK_GBS, "traffic": traffic,
                    "kernel": f"{kadj}<{Np},uniform,{tile_tag},{ms}{rec_tag}> ({ms} reverse steps + DWR per launch)",
                    "launch_us": adj_launch_us, "launch_us_stats": stats(adj_us),
-                   "algorithmic_bytes": adj_bytes, "traffic_source": traffic_src},
+                   "algorithmic_bytes": adj_bytes, "traffic_source": traffic_src,
+                   "note": (None if args.record != "jumps" else
+                            "jump record: 16 B per element-step instead of an 8 Np B snapshot, so "
+                            "the launches are bound by fp64 issue and the per-stage barrier "
+                            "chain, not HBM (roofline_fp64); the snapshot sweep's k_adj reaches "
+                            "0.62 of HBM (--record snapshots, DESIGN.md section 7)")},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_gbs / HBM_PEAK_GBS,
                        "kernel": f"{kstep}<{Np},uniform,{tile_tag},{ms}{rec_tag}> ({ms} steps per launch)",
