@@ -64,3 +64,31 @@ def test_operator_refuses_cpu(pkg):
     pytest.skip("GPU present")
   with pytest.raises(pkg._lib.DGLibraryError):
     pkg.operators.DGAdvection1D(pkg.BaseGalerkin1D(n=2, k=8))
+
+
+def header_enums():
+  """name -> value of every `DG_NAME = value` enumerator in include/dg_advec.h."""
+  src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+  out = {}
+  for body in re.findall(r"enum\s*\{(.*?)\}", src, flags=re.S):
+    for name, val in re.findall(r"\b(DG_[A-Z0-9_]+)\s*=\s*(-?\d+)", body):
+      out[name] = int(val)
+  return out
+
+
+def test_python_constants_match_the_header(pkg):
+  """The ctypes layer's constants are the header's enumerators (a new tuning key or flag
+  added on one side only would pass the wrong integer across the ABI)."""
+  enums = header_enums()
+  assert len(enums) >= 20
+  for name, val in enums.items():
+    assert hasattr(pkg._lib, name), f"_lib lacks {name}"
+    assert getattr(pkg._lib, name) == val, name
+
+
+def test_tuning_a_null_plan_is_an_argument_error(pkg):
+  lib = pkg._lib.load()
+  for key in (pkg._lib.DG_TUNE_REC_LANE_ELEMENTS, pkg._lib.DG_TUNE_REC_STEPS_PER_LAUNCH):
+    assert lib.dg_plan_tune(None, key, 2) == pkg._lib.DG_ERR_ARG
+  out = (ctypes.c_int64 * 3)()
+  assert lib.dg_plan_query_rec(None, out) == pkg._lib.DG_ERR_ARG
