@@ -8,15 +8,17 @@
 //     reads half the LDS words per element and a barrier covers twice the elements;
 //   - the E independent element chains per lane give the fp64 pipe instruction-level
 //     parallelism between a stage's barrier and its update;
-//   - a 256*W-lane workgroup covers 256*W*E elements: the default (W = 1) puts a 512-element
-//     tile on 4 waves instead of 8, so each stage barrier waits for half as many waves;
+//   - a 256*W-lane workgroup covers 256*W*E elements: 512 per tile on 4 waves (W = 1) or
+//     1024 on 8 waves (W = 2, the default with 10 steps per launch: 41 KB of LDS, 3
+//     workgroups per CU);
 //   - the face arrays alias the staging image (one barrier after the image is read and one
-//     before it is rewritten, per launch): 20.8 KB of LDS per 512-element tile.
-// Measured (N = 4, K = 2^20, bench, A/B on one box): 5.86-5.98e11 DOF-updates/s against
-// 5.67-5.70e11 for the one-element-per-lane record kernels; 1024-element tiles (W = 2, 8-wave
-// workgroups, 3 per CU) 5.65-5.68e11 despite half the halo; 4 elements per lane 5.3e11;
-// raised wave priority on the post-barrier chain, an unrolled step loop, no scheduling pins:
-// all within noise.
+//     before it is rewritten, per launch);
+//   - launches of 5, 10, 16 or 20 steps (no one-element-per-lane counterpart).
+// Measured (N = 4, K = 2^20, bench, A/B pairs on one box, DESIGN.md §5 "Pair tiles"): with
+// 8 + 8 + 4 launches 5.86-5.98e11 DOF-updates/s on 512-element tiles against 5.67-5.72e11 for
+// the one-element-per-lane record kernels; 10 + 10 launches 6.07-6.12e11 (W = 1) and
+// 6.15-6.16e11 (W = 2, the default).  Four elements per lane, raised wave priority, an
+// unrolled step loop, no scheduling pins, 6 waves per SIMD for the adjoint: no gain.
 // Sources: AdvecRHS1D (utils/AdvecRHS1D.m:9-19), the LSERK4 loop (utils/One_code.mlx:106-140),
 // the indicator pattern (python/Main_finite_difference.py:54-94); DESIGN.md §5.
 #include "dg_common.h"
