@@ -20,7 +20,7 @@ DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
 DG_TUNE_TILE_WIDTH, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
 DG_TUNE_LANE_ELEMENTS = 4
 DG_TUNE_REC_TILE_WIDTH, DG_TUNE_REC_STEPS_PER_LAUNCH = 5, 6
-DG_TUNE_REC_LANE_ELEMENTS = 7
+DG_TUNE_REC_LANE_ELEMENTS, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 7, 8
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2

@@ -105,11 +105,12 @@ class DGAdvection1D:
     self.stages = int(q[5])
     self.tile_width = int(q[6])
     self.steps_per_launch = int(q[7])
-    r = (ctypes.c_int64 * 3)()
+    r = (ctypes.c_int64 * 4)()
     _lib.check(self._lib.dg_plan_query_rec(self._plan, r), "dg_plan_query_rec")
     self.rec_tile_width = int(r[0])  # the jump-record sweeps' shape
     self.rec_steps_per_launch = int(r[1])
     self.rec_lane_elements = int(r[2])
+    self.rec_fwd_steps_per_launch = int(r[3])
 
   # --- lifetime ---
   def close(self):
@@ -130,7 +131,8 @@ class DGAdvection1D:
     self.close()
 
   def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None,
-           rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None):
+           rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
+           rec_fwd_steps_per_launch=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -139,10 +141,13 @@ class DGAdvection1D:
     in even/odd coordinates between fused steps).  ``rec_tile_width`` (1, 2) and
     ``rec_steps_per_launch`` shape the jump-record sweeps (``forward_rec``/``adjoint_rec``);
     ``rec_lane_elements`` = 2 runs them with two consecutive elements per lane (tiles of
-    512*``rec_tile_width`` elements, bit-identical at equal steps per launch)."""
+    512*``rec_tile_width`` elements, bit-identical at equal steps per launch);
+    ``rec_fwd_steps_per_launch`` gives the forward its own steps per launch (setting
+    ``rec_steps_per_launch`` applies to both directions and clears it)."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
-                     (_lib.DG_TUNE_REC_LANE_ELEMENTS, rec_lane_elements)):
+                     (_lib.DG_TUNE_REC_LANE_ELEMENTS, rec_lane_elements),
+                     (_lib.DG_TUNE_REC_FWD_STEPS_PER_LAUNCH, rec_fwd_steps_per_launch)):
       if val is not None:
         _lib.check(self._lib.dg_plan_tune(self._plan, key, int(val)), "dg_plan_tune")
     if xcd_order is not None:

@@ -523,10 +523,11 @@ def main(argv=None):
     ms, tw = sweep.op.rec_steps_per_launch, sweep.op.rec_tile_width
   else:
     ms, tw = sweep.op.steps_per_launch, sweep.op.tile_width
-  chunks = sweep_chunks(nsteps, ms)
-  launches = len(chunks)
-  fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / launches for e in evs]
-  adj_us = [e[1].elapsed_time(e[2]) * 1e3 / launches for e in evs]
+  # the forward may take its own steps per launch (record sweeps: one 20-step launch)
+  fms = sweep.op.rec_fwd_steps_per_launch if args.record == "jumps" else ms
+  chunks, fchunks = sweep_chunks(nsteps, ms), sweep_chunks(nsteps, fms)
+  fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / len(fchunks) for e in evs]
+  adj_us = [e[1].elapsed_time(e[2]) * 1e3 / len(chunks) for e in evs]
   step_ms = [evs[i][0].elapsed_time(evs[i + 1][0] if i + 1 < len(evs) else ev_end)
              for i in range(len(evs))]
   fwd_launch_us, adj_launch_us = float(np.mean(fwd_us)), float(np.mean(adj_us))
@@ -540,10 +541,10 @@ def main(argv=None):
   # A sweep's launches may differ in m (e.g. 8 + 8 + 4 at 20 steps); the per-launch figures
   # are the sweep's averages: achieved = sweep bytes / sweep time.
   if args.record == "jumps":
-    fwd_bytes = float(np.mean([(16.0 * Np + 16.0 * m) * ktot for m in chunks]))
+    fwd_bytes = float(np.mean([(16.0 * Np + 16.0 * m) * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 * Np + 16.0 * m + 16.0) * ktot for m in chunks]))
   else:
-    fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in chunks]))
+    fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
   rec_tag = ",jumps" if args.record == "jumps" else ""
   pairs = args.record == "jumps" and getattr(sweep.op, "rec_lane_elements", 1) == 2
@@ -568,7 +569,7 @@ def main(argv=None):
   # the snapshot algorithm moves for the same steps) -- an effective rate, not HBM traffic.
   effective = None
   if args.record == "jumps":
-    snap_fwd = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in chunks]))
+    snap_fwd = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
     snap_adj = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
     eff_adj = snap_adj / (adj_launch_us * 1e-6) / 1e9
     eff_fwd = snap_fwd / (fwd_launch_us * 1e-6) / 1e9
@@ -589,8 +590,9 @@ def main(argv=None):
   dist_world = dist.get_world_size() if dist.is_initialized() else 1
   idx_ranks = ranks_agree(ref_idx, world, dev, args.backend)
   upl = Np * ktot * float(np.mean(chunks))  # DOF-updates per launch (sweep average)
+  fupl = Np * ktot * float(np.mean(fchunks))
   adj_tf = eo_flops_per_update(Np, True) * upl / (adj_launch_us * 1e-6) / 1e12
-  fwd_tf = eo_flops_per_update(Np, False) * upl / (fwd_launch_us * 1e-6) / 1e12
+  fwd_tf = eo_flops_per_update(Np, False) * fupl / (fwd_launch_us * 1e-6) / 1e12
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
       "value": value,
@@ -626,7 +628,7 @@ def main(argv=None):
                             "0.62 of HBM (--record snapshots, DESIGN.md section 7)")},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_gbs / HBM_PEAK_GBS,
-                       "kernel": f"{kstep}<{Np},uniform,{tile_tag},{ms}{rec_tag}> ({ms} steps per launch)",
+                       "kernel": f"{kstep}<{Np},uniform,{tile_tag},{fms}{rec_tag}> ({fms} steps per launch)",
                        "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
       "roofline_effective": effective,
@@ -655,6 +657,7 @@ def main(argv=None):
       "steps_per_launch": ms,
       "tile_width": tw,
       "launch_steps": chunks,
+      "launch_steps_fwd": fchunks,
       "refine_index": ref_idx,
       "refine_value": ref_val,
       "refine_index_ranks": idx_ranks,

@@ -92,25 +92,29 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *   DG_TUNE_REC_TILE_WIDTH    1 or 2: tile width of the jump-record sweeps
  *                             (dg_lserk4_fwd_rec / dg_lserk4_adj_rec): workgroups of 256*value
  *                             lanes (default 2)
- *   DG_TUNE_REC_STEPS_PER_LAUNCH  their steps per launch (default 10): 1, 2, 4, 5, 8, 10, 16
+ *   DG_TUNE_REC_STEPS_PER_LAUNCH  their steps per launch, both directions (default 10): 1, 2,
+ *                             4, 5, 8, 10, 16
  *                             or 20 on pair tiles (16 and 20 need tile width 2, else 8 / 10
  *                             are used), a sweep chunked by halving (20 -> 10 -> 5 -> 2 -> 1);
  *                             1, 2, 4 or 8 on one element per lane (8 needs tile width 2,
  *                             else 4); Np = 9 caps it at 2
+ *   DG_TUNE_REC_FWD_STEPS_PER_LAUNCH  the forward record sweep's own steps per launch (same
+ *                             values; default 20 on 1024-element pair tiles; setting
+ *                             DG_TUNE_REC_STEPS_PER_LAUNCH clears it to "as the adjoint")
  *   DG_TUNE_REC_LANE_ELEMENTS 1 or 2: consecutive elements per lane of the jump-record sweeps'
  *                             workgroup tiles (default 2: tiles of 512*width elements,
  *                             lane-internal faces in registers; Np <= 8; bit-identical to 1 at
  *                             equal steps per launch)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
- * DG_REC_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS. */
+ * DG_REC_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
-       DG_TUNE_REC_LANE_ELEMENTS = 7 };
+       DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
-/* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch,
- * out[2] = elements per lane. */
-int dg_plan_query_rec(const dg_plan* plan, int64_t out[3]);
+/* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
+ * (adjoint), out[2] = elements per lane, out[3] = the forward's steps per launch. */
+int dg_plan_query_rec(const dg_plan* plan, int64_t out[4]);
 
 /* Physics of the plan's steppers.  Default: DG_FLUX_LINEAR + DG_LIMIT_NONE (AdvecRHS1D).
  *   DG_FLUX_LINEAR      f(u) = a*u                               utils/AdvecRHS1D.m:9-19

@@ -90,5 +90,5 @@ def test_tuning_a_null_plan_is_an_argument_error(pkg):
   lib = pkg._lib.load()
   for key in (pkg._lib.DG_TUNE_REC_LANE_ELEMENTS, pkg._lib.DG_TUNE_REC_STEPS_PER_LAUNCH):
     assert lib.dg_plan_tune(None, key, 2) == pkg._lib.DG_ERR_ARG
-  out = (ctypes.c_int64 * 3)()
+  out = (ctypes.c_int64 * 4)()
   assert lib.dg_plan_query_rec(None, out) == pkg._lib.DG_ERR_ARG

@@ -304,3 +304,35 @@ def test_long_launch_shapes_are_checked(pkg, gpu):
   for bad in (3, 6, 12, 32):
     with pytest.raises(pkg._lib.DGLibraryError):
       op.tune(rec_steps_per_launch=bad)
+
+
+def test_forward_own_steps_per_launch(pkg, gpu):
+  """The forward record sweep's own steps per launch (DG_TUNE_REC_FWD_STEPS_PER_LAUNCH; the
+  default plan runs one 20-step forward launch and 10 + 10 adjoint launches): setting the
+  common value applies to both directions and clears the forward's; the default sweep agrees
+  with both directions at 10 steps to rounding (the state leaves even/odd coordinates at other
+  steps): u^N, w^0 and the record to 1e-12, eta to its conditioning."""
+  import torch
+  N, K, nsteps = 4, 3000, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  assert (op.rec_steps_per_launch, op.rec_fwd_steps_per_launch) == (10, 20)
+  dt = mesh.cfl_dt()
+  u0 = op.new_field()
+  op.init_sine([1.0], [1.0], [0.0], out=u0)
+  gen = torch.Generator(device=u0.device).manual_seed(3)
+  u0 += 0.1 * torch.randn(u0.shape, dtype=u0.dtype, device=u0.device, generator=gen)  # resolved jumps
+  got = rec_sweep(op, u0, dt, nsteps)
+  op.tune(rec_steps_per_launch=10)
+  assert (op.rec_steps_per_launch, op.rec_fwd_steps_per_launch) == (10, 10)
+  ref = rec_sweep(op, u0, dt, nsteps)
+  scale = float(np.abs(host(u0)).max())
+  for name, a, b in zip(("record", "u^N", "w^0"), got[:3], ref[:3]):
+    np.testing.assert_allclose(a, b, rtol=0, atol=1e-12 * max(scale, np.abs(b).max()), err_msg=name)
+  np.testing.assert_allclose(got[3], ref[3], rtol=0, atol=1e-10 * np.abs(ref[3]).max())
+  op.tune(rec_fwd_steps_per_launch=5)
+  assert (op.rec_steps_per_launch, op.rec_fwd_steps_per_launch) == (10, 5)
+  with pytest.raises(pkg._lib.DGLibraryError):
+    op.tune(rec_fwd_steps_per_launch=3)
+  op.tune(rec_tile_width=1, rec_fwd_steps_per_launch=20)
+  assert op.rec_fwd_steps_per_launch == 10  # 20-step launches need 1024-element tiles
