@@ -1009,10 +1009,17 @@ inline int rec_msteps_cap(const dg_plan* p, int m) {
 // Adjoint (and, unless overridden, forward) record steps per launch.
 inline int rec_msteps(const dg_plan* p) { return rec_msteps_cap(p, p->rec_msteps); }
 
-// Forward record steps per launch: the forward-only setting if any (measured: one 20-step
-// forward launch beats 10 + 10 by ~5 % at N = 4, the adjoint prefers 10 + 10).
+// Forward record steps per launch.  By size (the default): one 20-step launch on 1024-element
+// pair tiles while a 10-step launch would be only ~1.5-4 rounds of workgroups (up to 3*2^20
+// elements: at K = 2^20 / 2^21 the forward is 5 / 2 % faster than 10 + 10), beyond that the
+// adjoint's setting (at 2^22 equal, at config 4's 67 M elements 10 + 10 is 3 % faster: the
+// wider halo outweighs the launch saved).  The adjoint prefers 10 + 10 at every size.
 inline int rec_msteps_fwd(const dg_plan* p) {
-  return rec_msteps_cap(p, p->rec_msteps_fwd ? p->rec_msteps_fwd : p->rec_msteps);
+  int m = p->rec_msteps_fwd;
+  if (m < 0)
+    m = (rec_pairs(p) && p->rec_tile_width == 2 && p->ktot <= (int64_t(3) << 20)) ? 20
+                                                                               : p->rec_msteps;
+  return rec_msteps_cap(p, m ? m : p->rec_msteps);
 }
 
 inline int rec_width(const dg_plan* p, int /*ms*/) { return p->rec_tile_width; }

@@ -442,7 +442,9 @@ struct dg_plan {
   // launch (a 20-step sweep is 10 + 10 launches)
   int rec_tile_width = 2;
   int rec_msteps = 10;
-  int rec_msteps_fwd = 20;  // the forward's own setting (0: as rec_msteps): one 20-step launch
+  // the forward's own record steps per launch: -1 by size (20 on 1024-element pair tiles up to
+  // 3*2^20 elements, else as rec_msteps), 0 as rec_msteps, > 0 explicit
+  int rec_msteps_fwd = -1;
   int rec_lane_elems = 2;  // 2: the pair tiles of dg_rec.hip (Np <= 8), 1: dg_advec.hip k_step/k_adj
   int xcd_order = 1;  // XCD-aware tile order
   int lane_elems = 0;  // 0: workgroup tiles (one element per lane); 2 or 4: wave tiles

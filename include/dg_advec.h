@@ -99,8 +99,9 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             1, 2, 4 or 8 on one element per lane (8 needs tile width 2,
  *                             else 4); Np = 9 caps it at 2
  *   DG_TUNE_REC_FWD_STEPS_PER_LAUNCH  the forward record sweep's own steps per launch (same
- *                             values; default 20 on 1024-element pair tiles; setting
- *                             DG_TUNE_REC_STEPS_PER_LAUNCH clears it to "as the adjoint")
+ *                             values; default by size: 20 on 1024-element pair tiles up to
+ *                             3*2^20 elements per plan, else as the adjoint; setting
+ *                             DG_TUNE_REC_STEPS_PER_LAUNCH makes it "as the adjoint")
  *   DG_TUNE_REC_LANE_ELEMENTS 1 or 2: consecutive elements per lane of the jump-record sweeps'
  *                             workgroup tiles (default 2: tiles of 512*width elements,
  *                             lane-internal faces in registers; Np <= 8; bit-identical to 1 at

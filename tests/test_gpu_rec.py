@@ -307,8 +307,9 @@ def test_long_launch_shapes_are_checked(pkg, gpu):
 
 
 def test_forward_own_steps_per_launch(pkg, gpu):
-  """The forward record sweep's own steps per launch (DG_TUNE_REC_FWD_STEPS_PER_LAUNCH; the
-  default plan runs one 20-step forward launch and 10 + 10 adjoint launches): setting the
+  """The forward record sweep's own steps per launch (DG_TUNE_REC_FWD_STEPS_PER_LAUNCH; a
+  default plan of up to 3*2^20 elements runs one 20-step forward launch and 10 + 10 adjoint
+  launches, a larger one 10 + 10 both ways): setting the
   common value applies to both directions and clears the forward's; the default sweep agrees
   with both directions at 10 steps to rounding (the state leaves even/odd coordinates at other
   steps): u^N, w^0 and the record to 1e-12, eta to its conditioning."""
@@ -336,3 +337,9 @@ def test_forward_own_steps_per_launch(pkg, gpu):
     op.tune(rec_fwd_steps_per_launch=3)
   op.tune(rec_tile_width=1, rec_fwd_steps_per_launch=20)
   assert op.rec_fwd_steps_per_launch == 10  # 20-step launches need 1024-element tiles
+  # the default is by size: one 20-step forward launch up to 3*2^20 elements per plan
+  big = pkg.operators.DGAdvection1D(pkg.BaseGalerkin1D(n=4, k=1 << 20), batch=4)
+  assert (big.rec_steps_per_launch, big.rec_fwd_steps_per_launch) == (10, 10)
+  del big
+  mid = pkg.operators.DGAdvection1D(pkg.BaseGalerkin1D(n=4, k=1 << 20), batch=3)
+  assert mid.rec_fwd_steps_per_launch == 20
