@@ -983,8 +983,9 @@ int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const 
   return rc;
 }
 
-// Shapes: W = 1 with 1..4 steps, W = 2 with 1..8; Np = 9: at most 2 steps.  (1024-element
-// tiles -- 16-wave workgroups, 74 KB of LDS -- measured 20 % slower at N = 4, 8 steps.)
+// Record sweeps run on pair tiles (dg_rec.hip) for Np <= 8.  The one-element-per-lane record
+// kernels below: W = 1 with 1..4 steps, W = 2 with 1..8; Np = 9: at most 2 steps (1024-element
+// one-element-per-lane tiles -- 16-wave workgroups, 74 KB of LDS -- measured 20 % slower).
 inline bool rec_pairs(const dg_plan* p) { return p->rec_lane_elems == 2 && p->NP <= 8; }
 
 // Record steps per launch: pair tiles take 1, 2, 4, 5, 8, 10, 16 or 20 (a sweep is chunked by
