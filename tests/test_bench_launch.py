@@ -68,3 +68,21 @@ def test_bench_arguments():
   assert (a.gpus, a.steps, a.warmup, a.config, a.backend) == (8, 20, 5, 2, "nccl")
   assert b.parse(["--config", "3"]).steps == 10
   assert b.launches_per_sweep(20, 4) == 5 and b.launches_per_sweep(7, 4) == 3
+
+
+def test_bench_accounting_helpers():
+  """The bench's launch chunking mirrors the library's halving (dg_advec.hip chunk_rec: a
+  20-step sweep at 10 per launch is 10 + 10, at 20 one launch, 17 at 10 is 10 + 5 + 2) and
+  the even/odd flop counts behind roofline_fp64 (53 forward, 57.4 adjoint flop
+  per DOF-update at N = 4; per element-stage 4 + 5 Np + 4 NE NO and 6 + 5 Np + 4 NE NO)."""
+  sys.path.insert(0, ROOT)
+  import bench
+  assert bench.sweep_chunks(20, 10) == [10, 10]
+  assert bench.sweep_chunks(20, 20) == [20]
+  assert bench.sweep_chunks(17, 10) == [10, 5, 2]
+  assert bench.sweep_chunks(20, 8) == [8, 8, 4]
+  assert bench.sweep_chunks(23, 16) == [16, 4, 2, 1]
+  assert bench.eo_flops_per_update(5, False) == 53.0
+  assert abs(bench.eo_flops_per_update(5, True) - 57.4) < 1e-12
+  for Np in range(2, 10):  # fewer flops than SURVEY 8d's dense count 5 (2 Np + 11)
+    assert bench.eo_flops_per_update(Np, False) < 5 * (2 * Np + 11)
