@@ -15,12 +15,13 @@ HEADER_PATH = os.path.normpath(os.path.join(_HERE, "..", "include", "dg_advec.h"
 
 # Enumerations of include/dg_advec.h
 DG_OK, DG_ERR_ARG, DG_ERR_HIP, DG_ERR_NOMEM = 0, -1, -2, -3
-DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T = 0, 1
+DG_INFLOW_SIN_AT, DG_INFLOW_SIN_A2T, DG_INFLOW_ZERO = 0, 1, 2
 DG_TIME_LSERK4, DG_TIME_EULER = 0, 1
 DG_TUNE_TILE_WIDTH, DG_TUNE_STEPS_PER_LAUNCH, DG_TUNE_XCD_ORDER = 1, 2, 3
 DG_TUNE_LANE_ELEMENTS = 4
 DG_TUNE_REC_TILE_WIDTH, DG_TUNE_REC_STEPS_PER_LAUNCH = 5, 6
 DG_TUNE_REC_LANE_ELEMENTS, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 7, 8
+DG_TUNE_P_TILE_WIDTH, DG_TUNE_P_STEPS_PER_LAUNCH = 9, 10
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
@@ -56,6 +57,10 @@ SIGNATURES = {
                                  _vp]),
     "dg_lserk4_adj_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,
                                  _i32, _vp]),
+    "dg_plan_query_p": (_i32, [_vp, _vp]),
+    "dg_prolong": (_i32, [_vp, _vp, _c_dbl_p, _vp, _vp, _vp]),
+    "dg_lserk4_adj_p": (_i32, [_vp, _vp, _c_dbl_p, _vp, _vp, ctypes.c_double, ctypes.c_double,
+                               _i32, _vp, _i32, _vp]),
     "dg_slope_limit_n": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dg_slope_limit_1": (_i32, [_vp, _vp, _vp, _vp]),
     "dg_argmax": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),

@@ -11,7 +11,7 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(_HERE, "csrc", f) for f in ("dg_advec.hip", "dg_burgers.hip", "dg_wave.hip", "dg_time.hip", "dg_fd.hip",
-                                                     "dg_util.hip", "dg_rec.hip")]
+                                                     "dg_util.hip", "dg_rec.hip", "dg_dwr.hip")]
 COMMON = os.path.join(_HERE, "csrc", "dg_common.h")
 INCLUDE = os.path.normpath(os.path.join(_HERE, "..", "include"))
 OUT = os.path.join(_HERE, "lib", "libdgadv.so")

@@ -32,13 +32,13 @@ namespace {
 using namespace dgk;
 
 template <int NP, int NS, bool UNI, int W, int MS, bool REC>
-__global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* __restrict__ uin,
+__global__ __launch_bounds__(kBlock * W) void k_step(const double* __restrict__ uin,
                                                      double* __restrict__ snap,
                                                      double* __restrict__ last,
                                                      const double* __restrict__ scale,
                                                      StepArgs<NP, NS, MS> args);
 template <int NP, int NS, bool UNI, int W, int MS, bool REC>
-__global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(const double* __restrict__ win,
+__global__ __launch_bounds__(kBlock * W) void k_adj(const double* __restrict__ win,
                                                     double* __restrict__ wout,
                                                     const double* __restrict__ snap,
                                                     double* __restrict__ eta,
@@ -207,24 +207,6 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
         }
       }
     }
-#ifdef DG_DIRECT_STORE  // experiment: each lane stores its element from registers, no LDS pass
-    if (!EDGE && (snap != nullptr || st == MS - 1)) {
-      if (E[0].valid) {
-        double u[NP];
-        from_eo<NP>(ev[0], od[0], u);
-        if (snap != nullptr) {
-          double* o = snap + st * args.stride + E[0].e * NP;
-#pragma unroll
-          for (int i = 0; i < NP; ++i) o[i] = u[i];
-        }
-        if (st == MS - 1 && last != nullptr) {
-#pragma unroll
-          for (int i = 0; i < NP; ++i) last[E[0].e * NP + i] = u[i];
-        }
-      }
-      continue;
-    }
-#endif
     if (REC && st == MS - 1 && args.jend) {
       // The sweep's final state u^{n0+MS}: one more face exchange (the buffer parity of the
       // stage after the last) for its jumps, record n0+MS-1; inflow at t_{n0+MS}.
@@ -258,7 +240,7 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
 }
 
 template <int NP, int NS, bool UNI, int W, int MS, bool REC>
-__global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* __restrict__ uin,
+__global__ __launch_bounds__(kBlock * W) void k_step(const double* __restrict__ uin,
                                                      double* __restrict__ snap,
                                                      double* __restrict__ last,
                                                      const double* __restrict__ scale,
@@ -266,9 +248,6 @@ __global__ __launch_bounds__(kBlock * W) DG_SGPR_ATTR void k_step(const double* 
   using G = TileGeo<NP, W>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * NS + 1];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
-#ifdef DG_SETPRIO_ODD  // experiment: desynchronise co-resident workgroups (MI355X_MICROARCH.md)
-  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
-#endif
   constexpr int H = MS * NS + (REC ? 1 : 0);
   const int64_t e0 = tile * (G::T - 2 * H) - H;
   if (edge_tile(e0, G::T, args.ktot, args.K))
@@ -512,7 +491,7 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 }
 
 template <int NP, int NS, bool UNI, int W, int MS, bool REC>
-__global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(const double* __restrict__ win,
+__global__ __launch_bounds__(kBlock * W) void k_adj(const double* __restrict__ win,
                                                     double* __restrict__ wout,
                                                     const double* __restrict__ snap,
                                                     double* __restrict__ eta,
@@ -521,9 +500,6 @@ __global__ __launch_bounds__(kBlock * W, DG_ADJ_MINW) DG_SGPR_ATTR void k_adj(co
   using G = TileGeo<NP, W>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS + 1];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
-#ifdef DG_SETPRIO_ODD  // experiment: desynchronise co-resident workgroups (MI355X_MICROARCH.md)
-  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
-#endif
   const int64_t e0 = tile * (G::T - 2 * MS * NS) - MS * NS;
   if (edge_tile(e0, G::T, args.ktot, args.K))
     adj_tile<NP, NS, UNI, W, MS, REC, true>(lds, tile, win, wout, snap, eta, scale, args);
@@ -1116,7 +1092,8 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   if (K * batch >= (int64_t(1) << 31) - 4096)
     return fail(DG_ERR_ARG, "batch*K must stay below 2^31 elements per plan");
   if (!r || !V || !invV || !Dr || !LIFT || !VX) return fail(DG_ERR_ARG, "null operator pointer");
-  if (inflow_variant != DG_INFLOW_SIN_AT && inflow_variant != DG_INFLOW_SIN_A2T)
+  if (inflow_variant != DG_INFLOW_SIN_AT && inflow_variant != DG_INFLOW_SIN_A2T &&
+      inflow_variant != DG_INFLOW_ZERO)
     return fail(DG_ERR_ARG, "bad inflow_variant");
   if (time_scheme != DG_TIME_LSERK4 && time_scheme != DG_TIME_EULER)
     return fail(DG_ERR_ARG, "bad time_scheme");
@@ -1192,7 +1169,11 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     }
     if (const char* v = std::getenv("DG_REC_STEPS_PER_LAUNCH")) {
       const int k = std::atoi(v);
-      if (rec_msteps_ok(k)) p->rec_msteps = k;
+      // both directions, as DG_TUNE_REC_STEPS_PER_LAUNCH (the forward's own override below)
+      if (rec_msteps_ok(k)) {
+        p->rec_msteps = k;
+        p->rec_msteps_fwd = 0;
+      }
     }
     if (const char* v = std::getenv("DG_REC_FWD_STEPS_PER_LAUNCH")) {
       const int k = std::atoi(v);
@@ -1201,6 +1182,14 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     if (const char* v = std::getenv("DG_REC_LANE_ELEMENTS")) {
       const int k = std::atoi(v);
       if (k == 1 || k == 2) p->rec_lane_elems = k;
+    }
+    if (const char* v = std::getenv("DG_P_TILE_WIDTH")) {
+      const int k = std::atoi(v);
+      if (k == 1 || k == 2) p->p_tile_width = k;
+    }
+    if (const char* v = std::getenv("DG_P_STEPS_PER_LAUNCH")) {
+      const int k = std::atoi(v);
+      if (k == 1 || k == 2 || k == 4 || k == 8) p->p_msteps = k;
     }
   }
   auto cleanup = [&](const std::string& m) {
@@ -1259,9 +1248,25 @@ int dg_plan_query_rec(const dg_plan* p, int64_t out[4]) {
   return DG_OK;
 }
 
+int dg_plan_query_p(const dg_plan* p, int64_t out[2]) {
+  if (!p || !out) return fail(DG_ERR_ARG, "null argument");
+  out[0] = p->p_tile_width;
+  out[1] = (p->p_msteps == 8 && p->p_tile_width != 2) ? 4 : p->p_msteps;
+  return DG_OK;
+}
+
 int dg_plan_tune(dg_plan* p, int key, int64_t value) {
   if (!p) return fail(DG_ERR_ARG, "null plan");
   switch (key) {
+    case DG_TUNE_P_TILE_WIDTH:
+      if (value != 1 && value != 2) return fail(DG_ERR_ARG, "p-estimate tile width must be 1 or 2");
+      p->p_tile_width = int(value);
+      return DG_OK;
+    case DG_TUNE_P_STEPS_PER_LAUNCH:
+      if (value != 1 && value != 2 && value != 4 && value != 8)
+        return fail(DG_ERR_ARG, "p-estimate steps per launch must be 1, 2, 4 or 8");
+      p->p_msteps = int(value);
+      return DG_OK;
     case DG_TUNE_REC_TILE_WIDTH:
       if (value != 1 && value != 2)
         return fail(DG_ERR_ARG, "record tile width must be 1 or 2");
@@ -1558,7 +1563,9 @@ int dg_lserk4_fwd_rec(dg_plan* p, const double* u0, double* uN, double t0, doubl
 
 int dg_lserk4_adj_rec(dg_plan* p, double* w, const double* jumps, double t0, double dt,
                       int nsteps, double* eta, int flags, void* stream) {
-  if (!p || !w || (!jumps && eta && nsteps > 0)) return fail(DG_ERR_ARG, "null argument");
+  // the record is read by every reverse step (the kernels prefetch it whether or not eta is
+  // wanted), so it is required whenever there is a step to run
+  if (!p || !w || (!jumps && nsteps > 0)) return fail(DG_ERR_ARG, "null argument");
   if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
   if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS)) return fail(DG_ERR_ARG, "unknown flags");
   if (p->nonlinear() || p->nstages != 5)

@@ -385,7 +385,7 @@ template <int NP> struct NLAdjArgs {
 };
 
 template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN>
-__global__ __launch_bounds__(kBlock * kNLAdjW, DG_NL_ADJ_MINW) DG_NL_SGPR_ATTR void k_adj_nl(const double* __restrict__ win,
+__global__ __launch_bounds__(kBlock * kNLAdjW, kNLAdjMinWaves) void k_adj_nl(const double* __restrict__ win,
                                                    double* __restrict__ wout,
                                                    const double* __restrict__ snap,
                                                    double* __restrict__ eta,
@@ -693,7 +693,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
 }
 
 template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN>
-__global__ __launch_bounds__(kBlock * kNLAdjW, DG_NL_ADJ_MINW) DG_NL_SGPR_ATTR void k_adj_nl(const double* __restrict__ win,
+__global__ __launch_bounds__(kBlock * kNLAdjW, kNLAdjMinWaves) void k_adj_nl(const double* __restrict__ win,
                                                    double* __restrict__ wout,
                                                    const double* __restrict__ snap,
                                                    double* __restrict__ eta,

@@ -25,30 +25,14 @@ constexpr int kBlock = 256;       // lanes per workgroup = elements per tile (in
 constexpr int kMaxNP = 9;         // N <= 8
 constexpr int kArgmaxParts = 1024;
 
-// SGPR budget of the hot step kernels.  The hardware admits 256-thread workgroups per CU up
-// to floor(800 / (ceil(sgpr/16)*16 + 16)) (MI355X_MICROARCH.md, Residency): 8 at <= 80
-// SGPRs, 7 at 82-96.  DG_SGPR_CAP caps the compiler's allocation (experiment knob).
-#ifdef DG_SGPR_CAP
-#define DG_SGPR_ATTR __attribute__((amdgpu_num_sgpr(DG_SGPR_CAP)))
-#else
-#define DG_SGPR_ATTR
-#endif
-#ifndef DG_ADJ_MINW
-#define DG_ADJ_MINW 1
-#endif
-// The same for the config-3 kernels, and the minimum waves per SIMD k_adj_nl's register
-// allocation targets (experiment knobs).
-#ifdef DG_NL_SGPR_CAP
-#define DG_NL_SGPR_ATTR __attribute__((amdgpu_num_sgpr(DG_NL_SGPR_CAP)))
-#else
-#define DG_NL_SGPR_ATTR
-#endif
-// k_step_nl: capped at 80 SGPRs so 8 workgroups fit per CU (at 94-100 SGPRs the hardware
-// admits 6-7; the spills go to VGPR lanes, the kernel stays at <= 64 VGPRs).
+// Register budgets of the config-3 kernels.  The hardware admits 256-thread workgroups per CU
+// up to floor(800 / (ceil(sgpr/16)*16 + 16)) (MI355X_MICROARCH.md, Residency): 8 at <= 80
+// SGPRs, 7 at 82-96.  k_step_nl is capped at 80 SGPRs so 8 workgroups fit per CU (at 94-100
+// SGPRs the hardware admits 6-7; the spills go to VGPR lanes, the kernel stays at <= 64
+// VGPRs); k_adj_nl targets 5 waves per SIMD (<= 96 VGPRs, dg_burgers.hip).  (Caps on the
+// linear kernels' SGPRs and wave priority were measured and rejected)
 #define DG_NL_STEP_ATTR __attribute__((amdgpu_num_sgpr(80)))
-#ifndef DG_NL_ADJ_MINW
-#define DG_NL_ADJ_MINW 5  // k_adj_nl: <= 96 VGPRs, 5 waves per SIMD (dg_burgers.hip)
-#endif
+constexpr int kNLAdjMinWaves = 5;
 
 // Indicator write mode of the adjoint kernels (the `has_eta` argument field):
 // bit 0 an indicator is wanted; bit 1 this launch assigns eta instead of adding to it (the
@@ -446,6 +430,10 @@ struct dg_plan {
   // 3*2^20 elements, else as rec_msteps), 0 as rec_msteps, > 0 explicit
   int rec_msteps_fwd = -1;
   int rec_lane_elems = 2;  // 2: the pair tiles of dg_rec.hip (Np <= 8), 1: dg_advec.hip k_step/k_adj
+  // the p-enriched estimate's shape (dg_lserk4_adj_p, dg_dwr.hip): tile width 1 or 2 (256 or
+  // 512 elements), steps per launch 1, 2, 4 or 8 (8 on 512-element tiles)
+  int p_tile_width = 2;
+  int p_msteps = 4;
   int xcd_order = 1;  // XCD-aware tile order
   int lane_elems = 0;  // 0: workgroup tiles (one element per lane); 2 or 4: wave tiles
   // physics (dg_plan_set_physics): DG_FLUX_LINEAR / DG_FLUX_BURGERS, SlopeLimitN per stage
@@ -457,6 +445,7 @@ struct dg_plan {
 namespace dgk {
 
 inline double inflow_value(const dg_plan* p, double t) {
+  if (p->inflow == DG_INFLOW_ZERO) return 0.0;
   return (p->inflow == DG_INFLOW_SIN_A2T) ? -std::sin(p->a * p->a * t) : -std::sin(p->a * t);
 }
 

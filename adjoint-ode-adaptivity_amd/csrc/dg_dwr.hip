@@ -1,0 +1,560 @@
+// dg_dwr.hip — the p-enriched dual-weighted-residual ERROR ESTIMATE of SURVEY 8(a) row 8
+// (dg_prolong / dg_lserk4_adj_p).
+//
+// The reference's indicator is an error estimate: matlab/MAIN.m:32-34 marches the primal at
+// order Ns and the adjoint at order Ns+1, and adj_march.m:103-117 pairs that adjoint with the
+// primal's residual, err(k) = v_k' (-A uh_k - M~ + F); python/Main_finite_difference.py:79-94
+// ("the Adjoint-Weighted Residual as an error estimate") takes the one-step residual
+// res[n] = u_f[n] - Phi(u_f[n-1]) of the interpolated (refined) state.  For the DG advection
+// sweep the same construction, p-refined, is:
+//   P        interpolation of the order-N element polynomials to the order-(N+1) LGL nodes
+//   R^n      = P u^{n+1} - S_{N+1}(P u^n, t_n)       one-step residual of the enriched scheme
+//   w^{n+1}  the order-(N+1) discrete adjoint (terminal weight g = dJ_{N+1}/du)
+//   eta_k    = - sum_n  w^{n+1} . R^n   on element k
+// For the linear (affine) step e^{n+1} = A e^n - R^n with e = u_{N+1} - P u_h, so
+// sum_k eta_k = g . e^N = J_{N+1}(u_{N+1}) - J_{N+1}(P u_h) exactly for a linear J (the DWR
+// identity; CPU statement oracle/effectivity.py p_indicator).
+//
+// k_adj_p fuses the whole estimate into the order-(N+1) adjoint launch.  Per reverse step it
+// stages the order-N snapshot u^n (one tile, 16-byte loads, prefetched a step ahead),
+// prolongs each lane's element in even/odd coordinates (P is block diagonal there: LGL nodes
+// are symmetric), recomputes S_{N+1}(P u^n) with 5 forward stages on the tile (the cone is 5
+// elements per side, inside the adjoint's own halo), forms R^n against P u^{n+1} kept in
+// registers from the previous step, accumulates -w.R, and runs the 5 reverse stages.  No
+// prolonged field is ever stored: HBM sees the order-N snapshots once, w^{n0+MS} and w^{n0}
+// at order N+1, and eta.
+#include "dg_common.h"
+
+namespace dgk {
+
+// Prolongation in even/odd coordinates: e_hi = Pe e_lo, o_hi = Po o_lo.
+template <int NPL> struct PrEO {
+  static constexpr int NPH = NPL + 1;
+  static constexpr int NEL = (NPL + 1) / 2, NOL = NPL / 2;
+  static constexpr int NEH = (NPH + 1) / 2, NOH = NPH / 2;
+  double Pe[NEH * NEL];
+  double Po[NOH * NOL];
+};
+
+// Even/odd transform of an Np-node element (rows e_0..e_{NE-1}, o_0..o_{NO-1}) and its
+// inverse, as make_eo builds them (dg_common.h).
+inline void eo_matrices(int NP, double* T, double* Ti) {
+  const int NE = (NP + 1) / 2, NO = NP / 2, N = NP - 1;
+  for (int i = 0; i < NP * NP; ++i) T[i] = Ti[i] = 0.0;
+  for (int k = 0; k < NO; ++k) {
+    T[k * NP + k] += 0.5; T[k * NP + N - k] += 0.5;
+    T[(NE + k) * NP + k] += 0.5; T[(NE + k) * NP + N - k] -= 0.5;
+    Ti[k * NP + k] += 1.0; Ti[k * NP + NE + k] += 1.0;
+    Ti[(N - k) * NP + k] += 1.0; Ti[(N - k) * NP + NE + k] -= 1.0;
+  }
+  if (NE > NO) { T[NO * NP + NO] = 1.0; Ti[NO * NP + NO] = 1.0; }
+}
+
+// P (NPH x NPL, row-major: u_hi = P u_lo) -> its even/odd blocks.  False if P does not
+// commute with the node reversal to 1e-12 (nodes not symmetric).
+template <int NPL> bool make_prolong_eo(const double* P, PrEO<NPL>* out) {
+  constexpr int NPH = NPL + 1;
+  using R = PrEO<NPL>;
+  double Th[NPH * NPH], Tih[NPH * NPH], Tl[NPL * NPL], Til[NPL * NPL];
+  eo_matrices(NPH, Th, Tih);
+  eo_matrices(NPL, Tl, Til);
+  double TP[NPH * NPL], M[NPH * NPL];
+  double pmax = 0.0;
+  for (int i = 0; i < NPH; ++i)
+    for (int j = 0; j < NPL; ++j) {
+      double t = 0.0;
+      for (int k = 0; k < NPH; ++k) t += Th[i * NPH + k] * P[k * NPL + j];
+      TP[i * NPL + j] = t;
+      pmax = std::fmax(pmax, std::fabs(P[i * NPL + j]));
+    }
+  for (int i = 0; i < NPH; ++i)
+    for (int j = 0; j < NPL; ++j) {
+      double t = 0.0;
+      for (int k = 0; k < NPL; ++k) t += TP[i * NPL + k] * Til[k * NPL + j];
+      M[i * NPL + j] = t;
+    }
+  const double tol = 1e-12 * (pmax > 0.0 ? pmax : 1.0);
+  bool ok = pmax > 0.0;
+  for (int i = 0; i < NPH; ++i)
+    for (int j = 0; j < NPL; ++j) {
+      const bool even_row = i < R::NEH, even_col = j < R::NEL;
+      if (even_row != even_col) ok = ok && std::fabs(M[i * NPL + j]) <= tol;
+    }
+  if (out) {
+    for (int k = 0; k < R::NEH; ++k)
+      for (int j = 0; j < R::NEL; ++j) out->Pe[k * R::NEL + j] = M[k * NPL + j];
+    for (int k = 0; k < R::NOH; ++k)
+      for (int j = 0; j < R::NOL; ++j) out->Po[k * R::NOL + j] = M[(R::NEH + k) * NPL + R::NEL + j];
+  }
+  return ok;
+}
+
+}  // namespace dgk
+
+namespace {
+using namespace dgk;
+
+// Arguments of one k_adj_p launch (MS reverse steps n0+MS-1 .. n0).
+template <int NPL, int MS> struct AdjPArgs {
+  EOArgs<NPL + 1> op;        // the order-(N+1) operator, folded; dt*2/h folded on uniform meshes
+  PrEO<NPL> pr;
+  double sc;                 // dt (non-uniform meshes multiply by scale[k])
+  double uin[MS * 5 + 1];    // inflow at the forward stages of steps n0..n0+MS-1, then 0
+  int64_t ktot;
+  int64_t stride;            // doubles between consecutive order-N snapshots
+  int32_t K;
+  int32_t has_eta;           // kEta* bits
+  int32_t xcd;
+};
+
+template <int NPL, int W> struct PGeo {
+  static constexpr int NPH = NPL + 1;
+  static constexpr int LB = kBlock * W, T = LB;
+  static constexpr int kImgD = T * NPH + 2;  // the image holds the w tile or a snapshot tile
+  static constexpr int kFB = (kImgD + 1) & ~1;
+  static constexpr int kFaceD = 4 * (T + 2);  // two double-buffered face arrays, padded by 1
+  static constexpr int kLds = kFB + kFaceD;
+};
+
+template <int NPL>
+__device__ __forceinline__ void prolong_eo(const double* __restrict__ u, const PrEO<NPL>& pr,
+                                           double* ev, double* od) {
+  using R = PrEO<NPL>;
+  double el[R::NEL], ol[R::NOL];
+  to_eo<NPL>(u, el, ol);
+#pragma unroll
+  for (int k = 0; k < R::NEH; ++k) {
+    double t = pr.Pe[k * R::NEL] * el[0];
+#pragma unroll
+    for (int j = 1; j < R::NEL; ++j) t = fma(pr.Pe[k * R::NEL + j], el[j], t);
+    ev[k] = t;
+  }
+#pragma unroll
+  for (int k = 0; k < R::NOH; ++k) {
+    double t = pr.Po[k * R::NOL] * ol[0];
+#pragma unroll
+    for (int j = 1; j < R::NOL; ++j) t = fma(pr.Po[k * R::NOL + j], ol[j], t);
+    od[k] = t;
+  }
+}
+
+template <int NPL, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_adj_p(const double* __restrict__ win,
+                                                      double* __restrict__ wout,
+                                                      const double* __restrict__ snap,
+                                                      double* __restrict__ eta,
+                                                      const double* __restrict__ scale,
+                                                      AdjPArgs<NPL, MS> args);
+
+// One tile of a k_adj_p launch.  snap = u^{n0}; the launch reads u^{n0} .. u^{n0+MS}.
+template <int NPL, bool UNI, int W, int MS, bool EDGE>
+__device__ __forceinline__ void adjp_tile(double* __restrict__ lds, int64_t tile,
+                                          const double* __restrict__ win,
+                                          double* __restrict__ wout,
+                                          const double* __restrict__ snap,
+                                          double* __restrict__ eta,
+                                          const double* __restrict__ scale,
+                                          const AdjPArgs<NPL, MS>& args) {
+  constexpr int NPH = NPL + 1, NS = 5;
+  using G = PGeo<NPL, W>;
+  constexpr int T = G::T, LB = G::LB;
+  // The reverse cone is NS elements per step; the forward recompute of a step needs 5 more
+  // around the output elements, which the reverse halo of the steps still to come covers
+  // (H >= 5 for MS >= 1: the recompute is exact on [5, T-5) and the outputs lie in [H, T-H)).
+  constexpr int H = MS * NS;
+  constexpr int TE = T - 2 * H;
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int NE = EOArgs<NPH>::NE, NO = EOArgs<NPH>::NO, NH = NPH - 1;
+  const int lane = threadIdx.x;
+  const int64_t e0 = tile * TE - H;
+  const int64_t ndh = args.ktot * NPH, ndl = args.ktot * NPL;
+  constexpr int CB = G::kLds;  // lds[CB + st*NS + s]: stage inflow; lds[CB + MS*NS] = 0
+
+  TileRegs<NPH, W> pw;
+  TileRegs<NPL, W> pa, pb;
+  tile_issue<NPH, W, EDGE>(win, e0, ndh, pw);
+  tile_issue<NPL, W, EDGE>(snap + MS * args.stride, e0, ndl, pa);
+  tile_issue<NPL, W, EDGE>(snap + (MS - 1) * args.stride, e0, ndl, pb);
+  tile_commit<NPH, W>(pw, lds);
+  if constexpr (EDGE) {
+    using A = AdjPArgs<NPL, MS>;  // lane-indexed kernarg read, see step_tile (dg_advec.hip)
+    const double* ka = reinterpret_cast<const double*>(
+        kernarg_tail<decltype(&k_adj_p<NPL, UNI, W, MS>), A>() + offsetof(A, uin));
+    if (lane <= MS * NS) lds[CB + lane] = ka[lane];
+  }
+  __syncthreads();
+  double we[NE], wo[NO];  // the order-(N+1) adjoint in dual even/odd coordinates
+  {
+    const double* w = lds + pw.off + lane * NPH;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      we[k] = w[k] + w[NH - k];
+      wo[k] = w[k] - w[NH - k];
+    }
+    if constexpr (NE > NO) we[NO] = w[NO];
+  }
+  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  double sc = args.sc;
+  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
+  __syncthreads();  // the w image is read
+  tile_commit<NPL, W>(pa, lds);
+  __syncthreads();
+  double ne[NE], no[NO];  // P u^{n+1} of this lane's element
+  prolong_eo<NPL>(lds + pa.off + lane * NPL, args.pr, ne, no);
+  __syncthreads();
+  tile_commit<NPL, W>(pb, lds);
+  int off = pb.off;
+  __syncthreads();
+  double eacc = 0.0;
+
+#pragma unroll 1
+  for (int st = MS - 1; st >= 0; --st) {
+    // ---- P u^n, and the next snapshot's loads in flight behind this step ----
+    double ev[NE], od[NO], pn_e[NE], pn_o[NO];
+    prolong_eo<NPL>(lds + off + lane * NPL, args.pr, ev, od);
+#pragma unroll
+    for (int k = 0; k < NE; ++k) pn_e[k] = ev[k];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) pn_o[k] = od[k];
+    if (st > 0) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
+
+    // ---- S_{N+1}(P u^n): 5 forward stages (k_step's arithmetic at order N+1) ----
+    double re[NE], ro[NO];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      // face buffers alternate over the launch's global stage index (10 per step: even)
+      const int fL = G::kFB + (s & 1) * 2 * (T + 2), fR = fL + (T + 2);
+      const double u0 = ev[0] + od[0], uN = ev[0] - od[0];
+      lds[fL + lane + 1] = u0;
+      lds[fR + lane + 1] = uN;
+      __builtin_amdgcn_sched_barrier(0);
+      double pe[NE], po[NO];
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        double t = (UNI && s > 0) ? RK<NS>::A(s) * re[k] : args.op.Qeo[k * NO] * od[0];
+#pragma unroll
+        for (int j = (UNI && s > 0) ? 0 : 1; j < NO; ++j) t = fma(args.op.Qeo[k * NO + j], od[j], t);
+        pe[k] = t;
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        double t = (UNI && s > 0) ? RK<NS>::A(s) * ro[k] : args.op.Qoe[k * NE] * ev[0];
+#pragma unroll
+        for (int j = (UNI && s > 0) ? 0 : 1; j < NE; ++j) t = fma(args.op.Qoe[k * NE + j], ev[j], t);
+        po[k] = t;
+      }
+#pragma unroll
+      for (int k = 0; k < NE; ++k) pin(pe[k]);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) pin(po[k]);
+      __syncthreads();
+      // a trajectory's first element reads the inflow, its last one its own right node
+      const int iL = EDGE && E.first ? CB + st * NS + s : fR + lane;
+      const int iR = EDGE && E.last ? fR + lane + 1 : fL + lane + 2;
+      const double uL = lds[iL], uR = lds[iR];
+      const double dlt = uR - uL, sig = -(uL + uR);
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        if constexpr (UNI) {
+          re[k] = fma(args.op.le[k], dlt, pe[k]);
+        } else {
+          const double a = sc * fma(args.op.le[k], dlt, pe[k]);
+          re[k] = (s == 0) ? a : fma(RK<NS>::A(s), re[k], a);
+        }
+        ev[k] = fma(RK<NS>::B(s), re[k], ev[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        if constexpr (UNI) {
+          ro[k] = fma(args.op.lo[k], sig, po[k]);
+        } else {
+          const double a = sc * fma(args.op.lo[k], sig, po[k]);
+          ro[k] = (s == 0) ? a : fma(RK<NS>::A(s), ro[k], a);
+        }
+        od[k] = fma(RK<NS>::B(s), ro[k], od[k]);
+      }
+    }
+
+    // ---- eta -= w^{n+1} . (P u^{n+1} - S_{N+1}(P u^n)) in dual x primal even/odd ----
+    if (args.has_eta) {
+      double c = 0.0;
+#pragma unroll
+      for (int k = 0; k < NE; ++k) c = fma(we[k], ne[k] - ev[k], c);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) c = fma(wo[k], no[k] - od[k], c);
+      eacc -= c;
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) ne[k] = pn_e[k];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) no[k] = pn_o[k];
+    // the image's readers (prolong above) are 5 stage barriers behind
+    if (st > 0) {
+      tile_commit<NPL, W>(pa, lds);
+      off = pa.off;
+    }
+
+    // ---- w^n = S_{N+1}^T w^{n+1}: 5 reverse stages (k_adj's arithmetic at order N+1) ----
+    double le_[NE], lo_[NO];
+#pragma unroll
+    for (int k = 0; k < NE; ++k) le_[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) lo_[k] = 0.0;
+#pragma unroll
+    for (int ss = 0; ss < NS; ++ss) {
+      const int s = NS - 1 - ss;
+      const int f0 = G::kFB + ((NS + ss) & 1) * 2 * (T + 2), f1 = f0 + (T + 2);
+      double qe[NE], qo[NO];
+      double gd = 0.0, gs = 0.0;
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        le_[k] = fma(RK<NS>::B(s), we[k], le_[k]);
+        qe[k] = UNI ? le_[k] : sc * le_[k];
+        gd = fma(args.op.le[k], qe[k], gd);
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        lo_[k] = fma(RK<NS>::B(s), wo[k], lo_[k]);
+        qo[k] = UNI ? lo_[k] : sc * lo_[k];
+        gs = fma(args.op.lo[k], qo[k], gs);
+      }
+      const double g0 = gd + gs, g1 = gs - gd;
+      lds[f0 + lane + 1] = g0;
+      lds[f1 + lane + 1] = g1;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NE; ++j) {
+        double t = we[j];
+#pragma unroll
+        for (int k = 0; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[k], t);
+        we[j] = t;
+      }
+#pragma unroll
+      for (int j = 0; j < NO; ++j) {
+        double t = wo[j];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[k], t);
+        wo[j] = t;
+      }
+#pragma unroll
+      for (int k = 0; k < NE; ++k) le_[k] = RK<NS>::A(s) * le_[k];
+#pragma unroll
+      for (int k = 0; k < NO; ++k) lo_[k] = RK<NS>::A(s) * lo_[k];
+#pragma unroll
+      for (int k = 0; k < NE; ++k) pin(we[k]);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) pin(wo[k]);
+      __syncthreads();
+      // nothing arrives at a trajectory's first element from the left (its uL is the
+      // inflow); its last element's uR is its own u_N (du1 = 0)
+      const double gl = lds[EDGE && E.first ? CB + MS * NS : f1 + lane];
+      const double gr = lds[EDGE && E.last ? f1 + lane + 1 : f0 + lane + 2];
+      we[0] -= gl + gr;
+      wo[0] += gr - gl;
+    }
+  }
+
+  if (args.has_eta && E.valid) eta_update(eta, E.e, eacc, args.has_eta);
+  {
+    const double(*pwe)[NE] = &we;
+    const double(*pwo)[NO] = &wo;
+    stage_out<NPH, W, H>(lds, pwe, pwo, true);  // the image's last reads are 5 barriers behind
+  }
+  __syncthreads();
+  const int64_t o0 = tile * TE * NPH;
+  if constexpr (EDGE) {
+    const int64_t rem = ndh - o0;
+    store_run<LB>(wout, o0, rem < int64_t(TE) * NPH ? rem : int64_t(TE) * NPH, lds);
+  } else {
+    store_full<TE * NPH, LB>(wout, o0, lds);
+  }
+}
+
+template <int NPL, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_adj_p(const double* __restrict__ win,
+                                                      double* __restrict__ wout,
+                                                      const double* __restrict__ snap,
+                                                      double* __restrict__ eta,
+                                                      const double* __restrict__ scale,
+                                                      AdjPArgs<NPL, MS> args) {
+  using G = PGeo<NPL, W>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  constexpr int H = MS * 5;
+  const int64_t e0 = tile * (G::T - 2 * H) - H;
+  if (edge_tile(e0, G::T, args.ktot, args.K))
+    adjp_tile<NPL, UNI, W, MS, true>(lds, tile, win, wout, snap, eta, scale, args);
+  else
+    adjp_tile<NPL, UNI, W, MS, false>(lds, tile, win, wout, snap, eta, scale, args);
+}
+
+// u_hi = P u_lo, one element per lane (the enriched terminal state / initial state).
+template <int NPL>
+__global__ __launch_bounds__(kBlock) void k_prolong(const double* __restrict__ u,
+                                                    double* __restrict__ uh, PrEO<NPL> pr,
+                                                    int64_t ktot) {
+  constexpr int NPH = NPL + 1;
+  const int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (e >= ktot) return;
+  double ul[NPL], ev[EOArgs<NPH>::NE], od[EOArgs<NPH>::NO], out[NPH];
+#pragma unroll
+  for (int i = 0; i < NPL; ++i) ul[i] = u[e * NPL + i];
+  prolong_eo<NPL>(ul, pr, ev, od);
+  from_eo<NPH>(ev, od, out);
+#pragma unroll
+  for (int i = 0; i < NPH; ++i) uh[e * NPH + i] = out[i];
+}
+
+template <int NPL, int W, int MS>
+int launch_adj_p_e(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const double* win,
+                   double* wout, const double* snap, double* eta, int eta_mode,
+                   const double* tn, double dt, hipStream_t st) {
+  AdjPArgs<NPL, MS> a;
+  make_eo<NPL + 1>(hi, hi->uniform ? dt * hi->s_uniform : 1.0, &a.op, true);
+  a.pr = pr;
+  a.sc = dt;
+  for (int m = 0; m < MS; ++m)
+    for (int s = 0; s < 5; ++s) a.uin[m * 5 + s] = inflow_value(lo, tn[m] + RK<5>::C(s) * dt);
+  a.uin[MS * 5] = 0.0;
+  a.ktot = lo->ktot;
+  a.stride = lo->ktot * NPL;
+  a.K = int32_t(lo->K);
+  a.has_eta = eta != nullptr ? (eta_mode | kEtaOn) : 0;
+  a.xcd = lo->xcd_order;
+  constexpr int TE = kBlock * W - 2 * MS * 5;
+  const unsigned grid = grid_for(lo->ktot, TE);
+  if (hi->uniform)
+    hipLaunchKernelGGL((k_adj_p<NPL, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win, wout,
+                       snap, eta, hi->d_scale, a);
+  else
+    hipLaunchKernelGGL((k_adj_p<NPL, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win, wout,
+                       snap, eta, hi->d_scale, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+// Shapes: 256-element tiles with 1, 2 or 4 steps per launch; 512-element tiles with 2, 4 or 8.
+template <int NPL>
+int launch_adj_p_t(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, int ms,
+                   const double* win, double* wout, const double* snap, double* eta, int em,
+                   const double* tn, double dt, hipStream_t st) {
+  const bool w2 = lo->p_tile_width == 2;
+  if (w2 && ms == 8) return launch_adj_p_e<NPL, 2, 8>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
+  if (w2 && ms == 4) return launch_adj_p_e<NPL, 2, 4>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
+  if (w2 && ms == 2) return launch_adj_p_e<NPL, 2, 2>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
+  if (ms == 4) return launch_adj_p_e<NPL, 1, 4>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
+  if (ms == 2) return launch_adj_p_e<NPL, 1, 2>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
+  if (ms == 1) return launch_adj_p_e<NPL, 1, 1>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
+  return fail(DG_ERR_ARG, "p-estimate: unsupported steps per launch for this tile width");
+}
+
+// The estimate's steps per launch: the plan's setting (8 needs 512-element tiles), halved
+// until it fits the steps left.
+inline int p_msteps(const dg_plan* p) {
+  int m = p->p_msteps;
+  if (m == 8 && p->p_tile_width != 2) m = 4;
+  return m;
+}
+inline int chunk_p(const dg_plan* p, int left) {
+  int m = p_msteps(p);
+  while (m > left) m >>= 1;
+  return m < 1 ? 1 : m;
+}
+
+// Both plans describe one mesh and one problem (the order-(N+1) plan is the estimate's).
+int check_pair(const dg_plan* lo, const dg_plan* hi) {
+  if (hi->NP != lo->NP + 1) return fail(DG_ERR_ARG, "the enriched plan must have order N+1");
+  if (hi->K != lo->K || hi->batch != lo->batch)
+    return fail(DG_ERR_ARG, "the two plans differ in K or batch");
+  if (hi->a != lo->a || hi->inflow != lo->inflow)
+    return fail(DG_ERR_ARG, "the two plans differ in advection speed or inflow");
+  if (lo->nstages != 5 || hi->nstages != 5)
+    return fail(DG_ERR_ARG, "the p-estimate is the LSERK4 sweep's");
+  if (lo->nonlinear() || hi->nonlinear())
+    return fail(DG_ERR_ARG, "the p-estimate needs the linear flux without limiter");
+  if (hi->uniform != lo->uniform ||
+      (lo->uniform && std::fabs(hi->s_uniform - lo->s_uniform) > 1e-12 * lo->s_uniform))
+    return fail(DG_ERR_ARG, "the two plans are not on the same mesh");
+  return DG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_prolong(const dg_plan* lo, const dg_plan* hi, const double* P, const double* u,
+               double* u_hi, void* stream) {
+  if (!lo || !hi || !P || !u || !u_hi) return fail(DG_ERR_ARG, "null argument");
+  if (hi->NP != lo->NP + 1 || hi->ktot != lo->ktot)
+    return fail(DG_ERR_ARG, "the enriched plan must have order N+1 and the same elements");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int rc = DG_OK;
+  switch (lo->NP) {
+#define DG_PROLONG_CASE(NPLV)                                                               \
+    case NPLV: {                                                                            \
+      PrEO<NPLV> pr;                                                                        \
+      if (!make_prolong_eo<NPLV>(P, &pr))                                                   \
+        return fail(DG_ERR_ARG, "P does not commute with the node reversal (symmetric nodes)"); \
+      hipLaunchKernelGGL((k_prolong<NPLV>), dim3(grid_for(lo->ktot, kBlock)), dim3(kBlock), 0, \
+                         st, u, u_hi, pr, lo->ktot);                                        \
+      HIP_TRY(hipGetLastError());                                                           \
+    } break;
+    DG_PROLONG_CASE(2) DG_PROLONG_CASE(3) DG_PROLONG_CASE(4) DG_PROLONG_CASE(5)
+    DG_PROLONG_CASE(6) DG_PROLONG_CASE(7) DG_PROLONG_CASE(8)
+#undef DG_PROLONG_CASE
+    default: return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+  }
+  return rc;
+}
+
+int dg_lserk4_adj_p(dg_plan* lo, dg_plan* hi, const double* P, double* w, const double* snapshots,
+                    double t0, double dt, int nsteps, double* eta, int flags, void* stream) {
+  if (!lo || !hi || !P || !w || !snapshots) return fail(DG_ERR_ARG, "null argument");
+  if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
+  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS)) return fail(DG_ERR_ARG, "unknown flags");
+  if (int rc = check_pair(lo, hi)) return rc;
+  if (lo->NP > 8) return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (eta != nullptr && nsteps == 0 && (flags & DG_ADJ_ETA_ASSIGN))
+    HIP_TRY(hipMemsetAsync(eta, 0, sizeof(double) * lo->ktot, st));
+  if (nsteps == 0) return DG_OK;
+  const int64_t field_lo = lo->ktot * lo->NP, field_hi = hi->ktot * hi->NP;
+  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt, as the forward sweep
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  int launches = 0;
+  for (int n = nsteps; n > 0; n -= chunk_p(lo, n)) ++launches;
+  int l = 0;
+  const double* in = w;
+  for (int n = nsteps; n > 0; ++l) {  // this launch covers steps n-m .. n-1
+    const int m = chunk_p(lo, n);
+    const int n0 = n - m;
+    double* out = (l == launches - 1 && launches > 1)
+                      ? w : ((l % 2 == 0) ? hi->d_scratch : hi->d_scratch2);
+    const int em = ((l == 0 && (flags & DG_ADJ_ETA_ASSIGN)) ? kEtaAssign : 0) |
+                   ((n0 == 0 && (flags & DG_ADJ_ETA_ABS)) ? kEtaAbs : 0);
+    const double* snap = snapshots + int64_t(n0) * field_lo;
+    int rc = DG_OK;
+    switch (lo->NP) {
+#define DG_ADJP_CASE(NPLV)                                                                  \
+      case NPLV: {                                                                          \
+        PrEO<NPLV> pr;                                                                      \
+        if (!make_prolong_eo<NPLV>(P, &pr))                                                 \
+          return fail(DG_ERR_ARG, "P does not commute with the node reversal (symmetric nodes)"); \
+        rc = launch_adj_p_t<NPLV>(lo, hi, pr, m, in, out, snap, eta, em, &tn[n0], dt, st);   \
+      } break;
+      DG_ADJP_CASE(2) DG_ADJP_CASE(3) DG_ADJP_CASE(4) DG_ADJP_CASE(5)
+      DG_ADJP_CASE(6) DG_ADJP_CASE(7) DG_ADJP_CASE(8)
+#undef DG_ADJP_CASE
+      default: return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+    }
+    if (rc) return rc;
+    in = out;
+    n = n0;
+  }
+  if (in != w)  // a one-launch sweep went through scratch
+    HIP_TRY(hipMemcpyAsync(w, in, sizeof(double) * field_hi, hipMemcpyDeviceToDevice, st));
+  return DG_OK;
+}
+
+}  // extern "C"

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .operators import DGAdvection1D, sum_rows
+from .operators import DGAdvection1D, DWREstimate, sum_rows
 
 
 def ic_params(indices, seed_base=0):
@@ -50,23 +50,34 @@ class EnsembleSweep:
   """
 
   RECORDS = ("jumps", "snapshots")
+  INDICATORS = ("jump", "p")
 
   def __init__(self, mesh, ic_indices, nsteps, dt, a=2 * np.pi, inflow="a", seed_base=0,
-               params=None, record="jumps"):
+               params=None, record="jumps", indicator="jump"):
     self.ic_indices = list(ic_indices)
     self.batch = len(self.ic_indices)
     if self.batch < 1:
       raise ValueError("a rank needs at least one IC")
     if record not in self.RECORDS:
       raise ValueError(f"record must be one of {self.RECORDS}, got {record!r}")
+    if indicator not in self.INDICATORS:
+      raise ValueError(f"indicator must be one of {self.INDICATORS}, got {indicator!r}")
+    if indicator == "p" and record != "snapshots":
+      raise ValueError("the p-enriched estimate recomputes each step from the order-N "
+                       "snapshots: record='snapshots'")
     self.record = record
+    self.indicator = indicator
+    self.est = None
     self.nsteps, self.dt = int(nsteps), float(dt)
     self.op = DGAdvection1D(mesh, a=a, batch=self.batch, inflow=inflow)
     amp, freq, phase = params if params is not None else ic_params(self.ic_indices, seed_base)
     if record == "jumps":
       # The snapshot-free pair (dg_lserk4_fwd_rec / dg_lserk4_adj_rec): the forward keeps
       # per element and step only the two face jumps the indicator needs (16 B instead of
-      # 8 Np B); w, eta and the refine decision are bit-identical to the snapshot pair's.
+      # 8 Np B).  At equal steps per launch w, eta and the refine decision are bit-identical
+      # to the snapshot pair's; at the record pair's own (longer) launches the states differ
+      # in the last bits and eta by the indicator's conditioning (~1e-9 relative on smooth
+      # solutions, DESIGN.md §5 "The indicator's conditioning").
       self.u0 = self.op.new_field()
       self.op.init_sine(amp, freq, phase, out=self.u0)
       self.jumps = self.op.new_jumps(self.nsteps)
@@ -78,9 +89,15 @@ class EnsembleSweep:
       # u^0 lives in snapshot 0; the forward sweep with u aliasing it leaves it untouched.
       self.op.init_sine(amp, freq, phase, out=self.snaps[0])
       self.u0 = self.snaps[0]
-      # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
-      # place on snapshot N (the library allows that alias) and leaves dJ/du^0 there.
-      self.w = self.snaps[self.nsteps]
+      if indicator == "p":
+        # The p-enriched DWR estimate (dg_lserk4_adj_p): the adjoint runs
+        # at order N+1 from w = P u^N (J = |P u^N|^2 / 2 on the enriched nodes).
+        self.est = DWREstimate(self.op)
+        self.w = self.est.new_field()
+      else:
+        # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
+        # place on snapshot N (the library allows that alias) and leaves dJ/du^0 there.
+        self.w = self.snaps[self.nsteps]
     # per-IC |eta| rows; the adjoint's first launch assigns them (DG_ADJ_ETA_ASSIGN), so
     # they need no zero fill
     self.eta = torch.zeros(self.op.ktot, dtype=torch.float64, device=self.op.device)
@@ -99,12 +116,22 @@ class EnsembleSweep:
       self.op.forward(self.snaps[0], 0.0, self.dt, self.nsteps, self.snaps)
 
   def adjoint(self):
+    self.terminal()
     self.run_adjoint()
+
+  def terminal(self):
+    """The p-estimate's terminal weight w = P u^N (dg_prolong); nothing in the other modes
+    (their forward leaves u^N where the adjoint starts)."""
+    if self.est is not None:
+      self.est.prolong(self.snaps[self.nsteps], out=self.w)
 
   def run_adjoint(self):
     """The adjoint kernels: w^N -> w^0 in place and eta = |DWR| per IC row (assigned, not
     accumulated: no zero fill needed)."""
-    if self.record == "jumps":
+    if self.est is not None:
+      self.est.estimate(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta,
+                        eta_assign=True, eta_abs=True)
+    elif self.record == "jumps":
       self.op.adjoint_rec(self.w, self.jumps, 0.0, self.dt, self.nsteps, eta=self.eta,
                           eta_assign=True, eta_abs=True)
     else:

@@ -205,6 +205,14 @@ class BaseGalerkin1D:
     return np.asarray(v).reshape(-1, self.n_p).T.copy()
 
 
+def prolongation(lo, hi):
+  """P (hi.n_p x lo.n_p): the order-lo.n element polynomial through its nodal values,
+  evaluated at the order-hi.n LGL nodes (u_hi = P u_lo; Vandermonde1D.m at the new nodes
+  times invV).  The p-enrichment of the DWR estimate (MAIN.m:32-34 marches the adjoint one
+  order up; dg_lserk4_adj_p)."""
+  return lo.vandermonde1D(lo.n, hi.r_gl) @ lo.inv_v
+
+
 def split_interval(nodes, idx):
   """Insert the midpoint of interval ``idx`` (0-based) into a sorted node vector —
   the refinement of python/Main_finite_difference.py:336-341 (ref_idx = idx + 1) and

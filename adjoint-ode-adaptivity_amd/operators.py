@@ -29,9 +29,9 @@ import numpy as np
 import torch
 
 from . import _lib
-from .galerkin import BaseGalerkin1D
+from .galerkin import BaseGalerkin1D, prolongation
 
-INFLOW = {"a": _lib.DG_INFLOW_SIN_AT, "a2": _lib.DG_INFLOW_SIN_A2T}
+INFLOW = {"a": _lib.DG_INFLOW_SIN_AT, "a2": _lib.DG_INFLOW_SIN_A2T, "zero": _lib.DG_INFLOW_ZERO}
 SCHEME = {"lserk4": _lib.DG_TIME_LSERK4, "euler": _lib.DG_TIME_EULER}
 FLUX = {"linear": _lib.DG_FLUX_LINEAR, "burgers": _lib.DG_FLUX_BURGERS}
 LIMITER = {False: _lib.DG_LIMIT_NONE, True: _lib.DG_LIMIT_EACH_STAGE,
@@ -50,7 +50,8 @@ class DGAdvection1D:
       ``v_x`` are handed to the plan), or an int polynomial order together with ``v_x``.
     a: advection speed (One_code.mlx:116 uses 2*pi).
     batch: independent trajectories (ensemble ICs) sharing the mesh.
-    inflow: "a" (uin = -sin(a t), AdvecRHS1D.m:14) or "a2" (-sin(a^2 t), One_code.mlx:129).
+    inflow: "a" (uin = -sin(a t), AdvecRHS1D.m:14), "a2" (-sin(a^2 t), One_code.mlx:129) or
+      "zero" (uin = 0, the homogeneous problem).
     time_scheme: "lserk4" (Globals1D.m:19-34) or "euler".
     flux: "linear" (a*u, AdvecRHS1D) or "burgers" (a*u^2/2, build-defined, config 3).
     limiter: after every LSERK4 stage apply SlopeLimitN (True or "N", utils/SlopeLimitN.m)
@@ -357,6 +358,80 @@ class DGAdvection1D:
                                 self._field(out, "u"), _stream(self.device))
     _lib.check(rc, "dg_init_sine")
     return out
+
+
+class DWREstimate:
+  """The p-enriched dual-weighted-residual ERROR ESTIMATE of a linear LSERK4 plan (SURVEY
+  8(a) row 8; include/dg_advec.h ``dg_lserk4_adj_p``).
+
+  The reference estimates the error of its order-Ns solution with an adjoint marched one
+  order up (matlab/MAIN.m:32-34, adj_march.m:103-117: err(k) = v_k'(-A uh_k - M~ + F)) and
+  documents its FD variant as "the Adjoint-Weighted Residual as an error estimate"
+  (python/Main_finite_difference.py:79-94).  Here: P u_h prolongs the order-N snapshots to
+  order N+1, R^n = P u^{n+1} - S_{N+1}(P u^n) is the enriched scheme's one-step residual and
+  eta_k = -sum_n w^{n+1}_k . R^n_k with w the order-(N+1) discrete adjoint, so that
+  sum_k eta_k = J_{N+1}(u_{N+1}) - J_{N+1}(P u_h) for a linear functional (the DWR identity).
+
+  ``hi`` is the order-(N+1) plan on the lo plan's current mesh (its ``forward`` marches
+  u_{N+1} for the identity); ``P`` the prolongation (galerkin.prolongation)."""
+
+  def __init__(self, lo, tile_width=None, steps_per_launch=None):
+    if lo.flux != "linear" or lo.limiter or lo.time_scheme != "lserk4":
+      raise ValueError("the p-estimate is the linear LSERK4 sweep's")
+    if lo.N > 7:
+      raise ValueError("the p-estimate supports N <= 7 (the enriched plan needs N+1 <= 8)")
+    self.lo = lo
+    v_x = lo.v_x()  # the lo plan's current (possibly device-refined) mesh
+    mesh_lo = BaseGalerkin1D(n=lo.N, v_x=v_x)
+    self.mesh_hi = BaseGalerkin1D(n=lo.N + 1, v_x=v_x)
+    self.hi = DGAdvection1D(self.mesh_hi, a=lo.a, batch=lo.batch, inflow=lo.inflow,
+                            device=lo.device.index)
+    self.P = prolongation(mesh_lo, self.mesh_hi)
+    self._P, self._P_ptr = _lib.dbl_array(self.P)
+    self.tune(tile_width, steps_per_launch)
+
+  def tune(self, tile_width=None, steps_per_launch=None):
+    """Tiles of 256*``tile_width`` elements (1, 2) and ``steps_per_launch`` (1, 2, 4; 8 on
+    512-element tiles) reverse steps per launch of dg_lserk4_adj_p."""
+    lib, plan = self.lo._lib, self.lo._plan
+    if tile_width is not None:
+      _lib.check(lib.dg_plan_tune(plan, _lib.DG_TUNE_P_TILE_WIDTH, int(tile_width)), "dg_plan_tune")
+    if steps_per_launch is not None:
+      _lib.check(lib.dg_plan_tune(plan, _lib.DG_TUNE_P_STEPS_PER_LAUNCH, int(steps_per_launch)),
+                 "dg_plan_tune")
+    q = (ctypes.c_int64 * 2)()
+    _lib.check(lib.dg_plan_query_p(plan, q), "dg_plan_query_p")
+    self.tile_width, self.steps_per_launch = int(q[0]), int(q[1])
+    return self
+
+  def new_field(self, count=None):
+    return self.hi.new_field(count)
+
+  def prolong(self, u, out=None):
+    """P u: an order-N field (lo plan) to the order-(N+1) nodes (hi plan), on the device."""
+    out = self.hi.new_field() if out is None else out
+    rc = self.lo._lib.dg_prolong(self.lo._plan, self.hi._plan, self._P_ptr,
+                                 self.lo._field(u, "u"), self.hi._field(out, "out"),
+                                 _stream(self.lo.device))
+    _lib.check(rc, "dg_prolong")
+    return out
+
+  def estimate(self, w, snapshots, t0, dt, nsteps, eta=None, eta_assign=False, eta_abs=False):
+    """The estimate over the sweep the lo plan's ``forward`` wrote into ``snapshots``
+    ((nsteps+1) order-N fields): ``w`` (an order-(N+1) field, dJ_{N+1}/du at t_N) is swept
+    back in place to t_0 and eta (batch*K) receives -sum_n w^{n+1} . R^n per element
+    (``eta_assign``: assign instead of accumulate; ``eta_abs``: store |eta|)."""
+    eta_p = None if eta is None else self.lo._field(eta, "eta", self.lo.ktot)
+    flags = (_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) | (_lib.DG_ADJ_ETA_ABS if eta_abs else 0)
+    rc = self.lo._lib.dg_lserk4_adj_p(
+        self.lo._plan, self.hi._plan, self._P_ptr, self.hi._field(w, "w"),
+        self.lo._field(snapshots, "snapshots", (nsteps + 1) * self.lo.field_numel),
+        float(t0), float(dt), int(nsteps), eta_p, int(flags), _stream(self.lo.device))
+    _lib.check(rc, "dg_lserk4_adj_p")
+    return w, eta
+
+  def close(self):
+    self.hi.close()
 
 
 def stream_copy(src, dst):

@@ -20,6 +20,10 @@ trajectories, one per GPU (weak scaling; the only exchange is the indicator sum)
                                          every stage, K = 4,194,304, one refine iteration per step
                                          (fwd + adj + argmax + device split; replicas per GPU)
   python bench.py --N n                  BASELINE config 5 (polynomial-order sweep)
+  python bench.py --indicator p          the p-enriched DWR error estimate (SURVEY 8(a) row 8:
+                                         order-(N+1) adjoint + one-step residual of the
+                                         prolonged snapshots, dg_lserk4_adj_p) instead of the
+                                         jump indicator; forward with snapshots
 
 Multi-GPU: `--gpus N` without a launcher spawns N ranks itself (one process per GPU, before
 this process touches the GPU), each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1
@@ -50,6 +54,9 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector spec peak (AMD data sheet; not in 
 FP64_PROBE_TFLOPS = 64.6
 
 
+EPS = float(np.finfo(np.float64).eps)
+
+
 def eo_flops_per_update(Np, adjoint):
   """fp64 flops per DOF-update that the even/odd kernels execute for an interior element
   (per element-stage 4 + 5 Np + 4 NE NO forward; 6 + 5 Np + 4 NE NO reverse, plus
@@ -58,6 +65,24 @@ def eo_flops_per_update(Np, adjoint):
   if not adjoint:
     return 5.0 * (4 + 5 * Np + 4 * NE * NO) / Np
   return (5.0 * (6 + 5 * Np + 4 * NE * NO) + 2 * Np + 2) / Np
+
+
+def p_flops_per_update(Np):
+  """fp64 flops per (order-N) DOF-update of k_adj_p (dg_dwr.hip) for an interior element: per
+  element-step the prolongation (even/odd transform + the two blocks), the order-(N+1)
+  forward step that recomputes S_{N+1}(P u^n), the residual pairing and the order-(N+1)
+  reverse step -- divided by the Np order-N DOFs the step advances."""
+  Nh = Np + 1
+  NEl, NOl, NEh, NOh = (Np + 1) // 2, Np // 2, (Nh + 1) // 2, Nh // 2
+  prolong = 4 * NOl + 2 * (NEh * NEl + NOh * NOl)
+  fwd = 5.0 * (4 + 5 * Nh + 4 * NEh * NOh)
+  rev = 5.0 * (6 + 5 * Nh + 4 * NEh * NOh)
+  return (prolong + fwd + 3 * Nh + rev) / Np
+
+
+def halo_factor(T, H):
+  """Lanes issued per useful lane of a tile of T elements whose launch writes T - 2 H."""
+  return T / float(T - 2 * H)
 PROFILE_TRAFFIC = {  # per-launch PMC traffic of the sweep kernels (profiles/r02/collect.sh)
     "jumps": os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
     "snapshots": os.path.join(ROOT, "profiles", "r02", "pmc_traffic_snapshots.json")}
@@ -92,7 +117,13 @@ def parse(argv=None):
   p.add_argument("--record", default="jumps", choices=("jumps", "snapshots"),
                  help="what the forward sweep keeps for the indicator: the two face jumps per "
                       "element and step (dg_lserk4_fwd_rec, default) or full snapshots "
-                      "(dg_lserk4_fwd); results are bit-identical")
+                      "(dg_lserk4_fwd); bit-identical at equal steps per launch, else equal to "
+                      "the indicator's conditioning (~1e-9 relative on smooth solutions)")
+  p.add_argument("--indicator", default="jump", choices=("jump", "p"),
+                 help="jump: the lifted interelement-jump indicator paired with the order-N "
+                      "adjoint (a refinement ranking, DESIGN.md 6c); p: the p-enriched DWR "
+                      "error estimate (order-(N+1) adjoint x one-step residual of the prolonged "
+                      "snapshots; implies --record snapshots)")
   p.add_argument("--no-cpu-baseline", action="store_true")
   p.add_argument("--cpu-steps", type=int, default=12, help="time steps of the CPU sample")
   p.add_argument("--graph", action="store_true",
@@ -105,6 +136,8 @@ def parse(argv=None):
     a.steps = 10 if a.config == 3 else 100
   if a.warmup is None:
     a.warmup = 4 if a.config == 3 else 10
+  if a.indicator == "p":
+    a.record = "snapshots"
   return a
 
 
@@ -178,29 +211,45 @@ def stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
   return 2.0 * nbytes / float(np.median(ts)) / 1e9
 
 
-def cpu_baseline(N, K, nsteps, threads=1):
+def cpu_baseline(N, K, nsteps, threads=1, indicator="jump", ics=1, ics_total=1):
   """The oracle (numpy restatement of utils/*.m + One_code.mlx, vectorised like MATLAB,
   `threads` BLAS/OpenMP threads) on a bounded sample of the same workload: `nsteps`
-  forward + adjoint steps at the full N, K.  SURVEY §8d asks for 1 and 8 threads; only
-  the Dr/LIFT products are threaded by numpy, the elementwise passes stay serial."""
+  forward + adjoint steps at the full N, K, for `ics` of the workload's `ics_total`
+  trajectories (the oracle runs trajectories one after another, so its DOF-updates/s does
+  not depend on how many are sampled).  SURVEY §8d asks for 1 and 8 threads; only the
+  Dr/LIFT products are threaded by numpy, the elementwise passes stay serial.
+  indicator "p": the oracle's p-estimate (order-(N+1) residual + adjoint) instead of the
+  jump indicator."""
   from threadpoolctl import threadpool_limits
 
   from oracle import adjoint as oadj
   from oracle import advec as oadv
+  from oracle import effectivity as oef
   from oracle import setup1d
   S = setup1d.uniform_setup(N, K, metric="element")
+  S_hi = setup1d.uniform_setup(N + 1, K, metric="element") if indicator == "p" else None
   a = 2 * np.pi
   dt = oadv.bench_dt(S)
-  u0 = np.sin(2 * np.pi * S["x"])
   with threadpool_limits(threads):
     t0 = time.perf_counter()
-    snaps, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, a, S)
-    oadj.adjoint_sweep(snaps[-1], snaps, times, dt, a, S)
+    for j in range(ics):
+      u0 = np.sin(2 * np.pi * (j + 1) * S["x"])
+      snaps, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, a, S)
+      if indicator == "p":
+        P = oef.prolong_matrix(S, S_hi)
+        oef.p_estimate(snaps, times, dt, a, S, S_hi, P @ snaps[-1], inflow=oadv.INFLOW_A)
+      else:
+        oadj.adjoint_sweep(snaps[-1], snaps, times, dt, a, S)
     el = time.perf_counter() - t0
-  dofs = 2 * (N + 1) * K * nsteps
+  dofs = 2 * (N + 1) * K * nsteps * ics
+  what = "p-enriched DWR estimate" if indicator == "p" else "DWR jump indicator"
+  sample = (f"{nsteps} fwd + {nsteps} adj LSERK4 steps (with {what}) at N={N}, K={K}, "
+            f"numpy oracle, {threads} thread(s), {el:.1f} s")
+  if ics_total > 1:
+    sample += (f"; {ics} of the workload's {ics_total} trajectories (the oracle's time is "
+               f"linear in the trajectory count, so the rate stands for all of them)")
   return {"value": dofs / el, "unit": "DOF-updates/s", "cores": threads, "kind": "port",
-          "sample": f"{nsteps} fwd + {nsteps} adj LSERK4 steps (with DWR indicator) at N={N}, "
-                    f"K={K}, numpy oracle, {threads} thread(s), {el:.1f} s"}
+          "sample": sample}
 
 
 def cpu_baseline_config3(N, K, nsteps):
@@ -269,22 +318,40 @@ def stats(xs):
           "min": float(xs.min()), "max": float(xs.max())}
 
 
+def rank_device(backend, world, local, local_world, ndev):
+  """This rank's GPU index and its process-group arguments (None for one rank).  RCCL (the
+  torch "nccl" backend) runs one rank per GPU: the group is bound to this rank's device
+  (device_id, so RCCL sets up its communicator eagerly on that GPU), and more ranks on a node
+  than visible GPUs is refused here with a clear message -- RCCL itself would fail later with
+  a duplicate-GPU error.  gloo (tests: several ranks sharing one GPU) maps ranks round-robin."""
+  if ndev < 1:
+    raise RuntimeError("bench.py needs a ROCm GPU")
+  if world == 1:
+    return local % ndev, None
+  if backend == "nccl":
+    if local_world > ndev or local >= ndev:
+      raise RuntimeError(
+          f"RCCL needs one GPU per rank: {local_world} ranks on this node but {ndev} GPU(s) "
+          f"visible (local rank {local}); use --backend gloo to share a GPU between ranks")
+    return local, {"backend": "nccl", "device_id": local}
+  return local % ndev, {"backend": "gloo"}
+
+
 def init_dist(args):
   import torch
   import torch.distributed as dist
   world = int(os.environ.get("WORLD_SIZE", "1"))
   rank = int(os.environ.get("RANK", "0"))
   local = int(os.environ.get("LOCAL_RANK", "0"))
-  ndev = torch.cuda.device_count()
-  if ndev < 1:
-    raise RuntimeError("bench.py needs a ROCm GPU")
-  torch.cuda.set_device(local % ndev)
-  dev = torch.device("cuda", local % ndev)
-  if world > 1:
-    if args.backend == "nccl":
-      dist.init_process_group("nccl", device_id=dev)
+  local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+  idx, pg = rank_device(args.backend, world, local, local_world, torch.cuda.device_count())
+  torch.cuda.set_device(idx)
+  dev = torch.device("cuda", idx)
+  if pg is not None:
+    if "device_id" in pg:
+      dist.init_process_group(pg["backend"], device_id=dev)
     else:
-      dist.init_process_group("gloo")
+      dist.init_process_group(pg["backend"])
   return world, rank, dev
 
 
@@ -439,6 +506,30 @@ def launches_per_sweep(nsteps, ms):
   return len(sweep_chunks(nsteps, ms))
 
 
+def indicator_resolution(sweep, N, K):
+  """Is the indicator above its rounding floor?  Both indicators are built from interelement
+  differences of the states (the jumps u_0 - uL, u_N - uR); a smooth solution on a fine mesh
+  has jumps of O(h^{N+1}), which at config 2 (h = 2^-20) fall below the states' own rounding
+  (DESIGN.md §5 "The indicator's conditioning").  Reported: the largest jump relative to
+  max|u|, in units of eps; `resolved` when it exceeds 1e4 eps (four significant digits in the
+  largest jump; below that the refine index is decided by rounding)."""
+  import torch
+  with torch.no_grad():
+    if sweep.record == "jumps":
+      jmax = float(sweep.jumps.abs().max())  # (du0 - du1, du0 + du1): |du| <= max of the two
+      umax = float(sweep.u0.abs().max())
+    else:
+      # the jump indicator's adjoint runs in place on snapshot N; u^{N-1} is intact
+      u = sweep.snaps[sweep.nsteps if sweep.est is not None else max(sweep.nsteps - 1, 0)]
+      u = u.view(sweep.batch, K, N + 1)
+      jmax = float((u[:, 1:, 0] - u[:, :-1, N]).abs().max())
+      umax = float(u.abs().max())
+  rel = jmax / umax if umax > 0 else 0.0
+  return {"max_jump_over_max_u": rel, "in_eps": rel / EPS, "resolved": bool(rel > 1e4 * EPS),
+          "what": "largest interelement jump of the states the indicator reads / max|u|; "
+                  "resolved above 1e4 eps"}
+
+
 def main(argv=None):
   args = parse(argv)
   if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -468,7 +559,8 @@ def main(argv=None):
     params = ((np.array([1.0]), np.array([1.0]), np.array([0.0])) if rank == 0
               else ens.ic_params([rank]))
     n_total = world
-  sweep = ens.EnsembleSweep(mesh, ics, nsteps, dt, params=params, record=args.record)
+  sweep = ens.EnsembleSweep(mesh, ics, nsteps, dt, params=params, record=args.record,
+                            indicator=args.indicator)
   reducer = ens.DeviceReducer(sweep.op)  # argmax + value + non-finite count on the device
   if args.graph:
     sweep.capture()  # each sweep becomes one HIP graph launch
@@ -481,6 +573,10 @@ def main(argv=None):
     sweep.forward_graph() if args.graph else sweep.forward()
     if ev:
       ev[1].record(stream)
+    if not args.graph:
+      sweep.terminal()  # the p-estimate's w = P u^N (dg_prolong); nothing otherwise
+    if ev:
+      ev[3].record(stream)
     sweep.adjoint_graph() if args.graph else sweep.run_adjoint()
     if ev:
       ev[2].record(stream)
@@ -498,7 +594,7 @@ def main(argv=None):
   barrier(world)
   torch.cuda.synchronize()
 
-  evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+  evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
   ev_end = torch.cuda.Event(enable_timing=True)
   t0 = time.perf_counter()
   for s in range(args.steps):
@@ -519,15 +615,18 @@ def main(argv=None):
   pkg.adaptive.check_indicator(ref_val, ref_idx)
 
   Np, ktot = N + 1, K * sweep.batch
+  pmode = args.indicator == "p"
   if args.record == "jumps":
     ms, tw = sweep.op.rec_steps_per_launch, sweep.op.rec_tile_width
+    fms = sweep.op.rec_fwd_steps_per_launch  # the forward's own (one 20-step launch)
   else:
-    ms, tw = sweep.op.steps_per_launch, sweep.op.tile_width
-  # the forward may take its own steps per launch (record sweeps: one 20-step launch)
-  fms = sweep.op.rec_fwd_steps_per_launch if args.record == "jumps" else ms
+    fms = sweep.op.steps_per_launch
+    ms, tw = ((sweep.est.steps_per_launch, sweep.est.tile_width) if pmode
+              else (fms, sweep.op.tile_width))
   chunks, fchunks = sweep_chunks(nsteps, ms), sweep_chunks(nsteps, fms)
   fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / len(fchunks) for e in evs]
-  adj_us = [e[1].elapsed_time(e[2]) * 1e3 / len(chunks) for e in evs]
+  adj_us = [e[3].elapsed_time(e[2]) * 1e3 / len(chunks) for e in evs]
+  prolong_us = [e[1].elapsed_time(e[3]) * 1e3 for e in evs] if pmode else None
   step_ms = [evs[i][0].elapsed_time(evs[i + 1][0] if i + 1 < len(evs) else ev_end)
              for i in range(len(evs))]
   fwd_launch_us, adj_launch_us = float(np.mean(fwd_us)), float(np.mean(adj_us))
@@ -540,20 +639,41 @@ def main(argv=None):
   #     16 B per DOF + (16 m + 16) B per element.
   # A sweep's launches may differ in m (e.g. 8 + 8 + 4 at 20 steps); the per-launch figures
   # are the sweep's averages: achieved = sweep bytes / sweep time.
+  #   p-estimate (k_adj_p): reads w^{n+m} and writes w^n at order N+1 (16 (Np + 1) B per
+  #     element), reads the m + 1 order-N snapshots u^n..u^{n+m} (8 (m + 1) Np B), updates eta.
   if args.record == "jumps":
     fwd_bytes = float(np.mean([(16.0 * Np + 16.0 * m) * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 * Np + 16.0 * m + 16.0) * ktot for m in chunks]))
+  elif pmode:
+    fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
+    adj_bytes = float(np.mean([(16.0 * (Np + 1) + 8.0 * (m + 1) * Np + 16.0) * ktot
+                               for m in chunks]))
   else:
     fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
   rec_tag = ",jumps" if args.record == "jumps" else ""
   pairs = args.record == "jumps" and getattr(sweep.op, "rec_lane_elements", 1) == 2
   kadj, kstep = ("k_adj_rp", "k_step_rp") if pairs else ("k_adj", "k_step")
+  if pmode:
+    kadj = "k_adj_p"
   tile_tag = f"{tw},2 elements/lane" if pairs else f"{tw}"
+  # Issued vs useful lanes: each tile recomputes a halo of H elements per side (the
+  # dependency cone of its fused steps) and writes T - 2H, weighted by steps.
+  if args.record == "jumps":
+    T_adj = T_fwd = 256 * tw * (2 if pairs else 1)
+    h_fwd = lambda m: 5 * m + 1  # noqa: E731  (the final state's jumps need one more)
+  else:
+    T_adj = 256 * tw
+    # the snapshot forward runs on 256-element one-wave tiles (4 elements per lane) at N <= 2
+    # by default (dg_plan_create), else on workgroup tiles of 256 * tile width
+    T_fwd = 256 if N <= 2 else 256 * sweep.op.tile_width
+    h_fwd = lambda m: 5 * m  # noqa: E731
+  halo_adj = float(np.average([halo_factor(T_adj, 5 * m) for m in chunks], weights=chunks))
+  halo_fwd = float(np.average([halo_factor(T_fwd, h_fwd(m)) for m in fchunks], weights=fchunks))
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
-  if os.path.exists(PROFILE_TRAFFIC[args.record]):
+  if os.path.exists(PROFILE_TRAFFIC[args.record]) and not pmode:
     try:
       with open(PROFILE_TRAFFIC[args.record]) as f:
         tr = json.load(f)
@@ -583,16 +703,17 @@ def main(argv=None):
   # DOF-updates, so its HBM roofline is 8 TB/s / that per-update average.
   single_step_bytes = (16.0 + 24.0 + 16.0 / Np) / 2.0
   single_step_roofline = HBM_PEAK_GBS * 1e9 / single_step_bytes * world
-  # SURVEY §8d's algorithmic flop count, 5 (2 Np + 11) per DOF-update (both directions).
-  flop_per_update = 5.0 * (2 * Np + 11)
   copy_gbs = stream_copy_gbs(dev) if rank == 0 else None
   import torch.distributed as dist
   dist_world = dist.get_world_size() if dist.is_initialized() else 1
   idx_ranks = ranks_agree(ref_idx, world, dev, args.backend)
   upl = Np * ktot * float(np.mean(chunks))  # DOF-updates per launch (sweep average)
   fupl = Np * ktot * float(np.mean(fchunks))
-  adj_tf = eo_flops_per_update(Np, True) * upl / (adj_launch_us * 1e-6) / 1e12
-  fwd_tf = eo_flops_per_update(Np, False) * fupl / (fwd_launch_us * 1e-6) / 1e12
+  adj_fpu = p_flops_per_update(Np) if pmode else eo_flops_per_update(Np, True)
+  fwd_fpu = eo_flops_per_update(Np, False)
+  adj_tf = adj_fpu * upl / (adj_launch_us * 1e-6) / 1e12
+  fwd_tf = fwd_fpu * fupl / (fwd_launch_us * 1e-6) / 1e12
+  resolved = indicator_resolution(sweep, N, K)
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
       "value": value,
@@ -621,7 +742,10 @@ def main(argv=None):
                    "kernel": f"{kadj}<{Np},uniform,{tile_tag},{ms}{rec_tag}> ({ms} reverse steps + DWR per launch)",
                    "launch_us": adj_launch_us, "launch_us_stats": stats(adj_us),
                    "algorithmic_bytes": adj_bytes, "traffic_source": traffic_src,
-                   "note": (None if args.record != "jumps" else
+                   "traffic_from_profile": traffic is not None,
+                   "note": ("p-estimate: per reverse step the order-(N+1) forward step from the "
+                            "prolonged snapshot and the order-(N+1) reverse step (roofline_fp64)"
+                            if pmode else None if args.record != "jumps" else
                             "jump record: 16 B per element-step instead of an 8 Np B snapshot, so "
                             "the launches are bound by fp64 issue and the per-stage barrier "
                             "chain, not HBM (roofline_fp64); the snapshot sweep's k_adj reaches "
@@ -633,22 +757,23 @@ def main(argv=None):
                        "algorithmic_bytes": fwd_bytes},
       "roofline_effective": effective,
       # The compute roof of the same launches: the even/odd algorithm's fp64 flops (interior
-      # elements) / launch time, against the spec and the on-box FMA probe.
+      # elements) / launch time, against the spec and the on-box FMA probe; issued_frac
+      # counts the halo lanes each tile also computes (the work the lanes actually issue).
       "roofline_fp64": {
           "bound": "fp64 vector", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
           "probe_ceiling": FP64_PROBE_TFLOPS,
           "adj_achieved": adj_tf, "adj_frac": adj_tf / FP64_PEAK_TFLOPS,
           "fwd_achieved": fwd_tf, "fwd_frac": fwd_tf / FP64_PEAK_TFLOPS,
-          "flop_per_update": {"fwd": eo_flops_per_update(Np, False),
-                              "adj": eo_flops_per_update(Np, True)}},
+          "adj_halo_factor": halo_adj, "fwd_halo_factor": halo_fwd,
+          "adj_issued_frac": adj_tf * halo_adj / FP64_PEAK_TFLOPS,
+          "fwd_issued_frac": fwd_tf * halo_fwd / FP64_PEAK_TFLOPS,
+          "flop_per_update": {"fwd": fwd_fpu, "adj": adj_fpu},
+          "what": "algorithmic fp64 flops of the interior elements per launch / launch time; "
+                  "*_issued_frac multiplies by the tile's issued/useful lanes (halo)"},
       "step_ms_stats": stats(step_ms),
       "single_step_roofline": {"value": single_step_roofline, "unit": "DOF-updates/s",
                                "bytes_per_update": single_step_bytes,
                                "frac": value / single_step_roofline},
-      "flops": {"per_dof_update": flop_per_update,
-                "achieved_tflops": value * flop_per_update / 1e12,
-                "peak_fp64_vector_tflops_per_gpu": FP64_PEAK_TFLOPS,
-                "frac": value * flop_per_update / 1e12 / (FP64_PEAK_TFLOPS * world)},
       "stream_copy": {"achievable_GBs": copy_gbs, "unit": "GB/s",
                       "what": "dg_stream_copy (16 B per lane, 4 in flight) of 1 GiB, read + "
                               "write, rank 0",
@@ -658,19 +783,29 @@ def main(argv=None):
       "tile_width": tw,
       "launch_steps": chunks,
       "launch_steps_fwd": fchunks,
+      "indicator": args.indicator,
       "refine_index": ref_idx,
       "refine_value": ref_val,
       "refine_index_ranks": idx_ranks,
+      "indicator_resolved": resolved,
       "nonfinite_indicator_steps": nonfinite,
-      "collective_backend": args.backend if world > 1 else None,
-      "rccl_world_size": dist_world,
+      "dist_world_size": dist_world,
+      "collective_backend": (None if world == 1 else
+                             "rccl (torch nccl backend)" if args.backend == "nccl" else "gloo"),
       "host_issue_ms_per_step": host_issue / args.steps * 1e3,
+      "library": {"path": os.path.relpath(pkg._lib.LIB_PATH, ROOT),
+                  "override": bool(os.environ.get("DG_LIB_PATH"))},
   }
+  if pmode:
+    out["prolong_us"] = float(np.mean(prolong_us))
   if len(set(idx_ranks)) != 1:
     raise RuntimeError(f"refine index differs across ranks: {idx_ranks}")
-  if rank == 0 and world == 1 and args.ics == 0 and not args.no_cpu_baseline:
-    out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_steps)
-    out["cpu_baseline_8t"] = cpu_baseline(N, K, args.cpu_steps, threads=8)
+  if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    cs = args.cpu_steps if not pmode else max(2, args.cpu_steps // 2)
+    kw = dict(indicator=args.indicator, ics=min(2, n_total), ics_total=n_total)
+    out["cpu_baseline"] = cpu_baseline(N, K, cs, **kw)
+    if args.ics == 0:
+      out["cpu_baseline_8t"] = cpu_baseline(N, K, cs, threads=8, **kw)
   if rank == 0:
     print(json.dumps(out), flush=True)
   if world > 1:

@@ -41,8 +41,10 @@ enum {
 
 /* Inflow boundary value at x = 0.
  *   DG_INFLOW_SIN_AT : uin = -sin(a*t)    utils/AdvecRHS1D.m:14
- *   DG_INFLOW_SIN_A2T: uin = -sin(a*a*t)  utils/One_code.mlx:129 (the executed golden run) */
-enum { DG_INFLOW_SIN_AT = 0, DG_INFLOW_SIN_A2T = 1 };
+ *   DG_INFLOW_SIN_A2T: uin = -sin(a*a*t)  utils/One_code.mlx:129 (the executed golden run)
+ *   DG_INFLOW_ZERO   : uin = 0            the homogeneous problem (a pulse leaving the domain:
+ *                                         exact solution u0(x - a t); the effectivity study) */
+enum { DG_INFLOW_SIN_AT = 0, DG_INFLOW_SIN_A2T = 1, DG_INFLOW_ZERO = 2 };
 
 /* Time integrator of the forward step and of its discrete adjoint.
  *   DG_TIME_LSERK4: 5-stage low-storage RK4, coefficients utils/Globals1D.m:19-34
@@ -106,16 +108,25 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             workgroup tiles (default 2: tiles of 512*width elements,
  *                             lane-internal faces in registers; Np <= 8; bit-identical to 1 at
  *                             equal steps per launch)
+ *   DG_TUNE_P_TILE_WIDTH      1 or 2: tile width of the p-enriched estimate (dg_lserk4_adj_p):
+ *                             workgroups of 256*value lanes, one element per lane (default 2)
+ *   DG_TUNE_P_STEPS_PER_LAUNCH its steps per launch: 1, 2, 4 (default) or 8 (8 needs tile
+ *                             width 2, else 4); a sweep is chunked by halving
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
- * DG_REC_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS. */
+ * DG_REC_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
+ * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
-       DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8 };
+       DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
+       DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
  * (adjoint), out[2] = elements per lane, out[3] = the forward's steps per launch. */
 int dg_plan_query_rec(const dg_plan* plan, int64_t out[4]);
+
+/* The p-enriched estimate's effective shape: out[0] = tile width, out[1] = steps per launch. */
+int dg_plan_query_p(const dg_plan* plan, int64_t out[2]);
 
 /* Physics of the plan's steppers.  Default: DG_FLUX_LINEAR + DG_LIMIT_NONE (AdvecRHS1D).
  *   DG_FLUX_LINEAR      f(u) = a*u                               utils/AdvecRHS1D.m:9-19
@@ -215,11 +226,42 @@ int dg_lserk4_adj_ex(dg_plan* plan, double* w, const double* snapshots, double t
  *   jumps (device, 16-byte aligned, 2*nsteps*batch*K doubles): for n = 1..nsteps and element
  *   e, jumps[2*((n-1)*batch*K + e) + {0, 1}] = {du0 - du1, du0 + du1} of u^n at t_n.
  * dg_lserk4_adj_rec: dg_lserk4_adj_ex(w, snapshots, src_coef = 0, eta, flags) with the
- *   record of the same sweep in place of the snapshots (jumps may be null if eta is). */
+ *   record of the same sweep in place of the snapshots (required whenever nsteps > 0, also
+ *   without eta: DG_ERR_ARG otherwise). */
 int dg_lserk4_fwd_rec(dg_plan* plan, const double* u0, double* uN, double t0, double dt,
                       int nsteps, double* jumps, void* stream);
 int dg_lserk4_adj_rec(dg_plan* plan, double* w, const double* jumps, double t0, double dt,
                       int nsteps, double* eta, int flags, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * The p-enriched dual-weighted-residual ERROR ESTIMATE.  The reference
+ * marches the adjoint one order above the primal and pairs it with the primal's residual:
+ * matlab/MAIN.m:32-34 (dg_march(Ns), adj_march(Ns+1)), matlab/adj_march.m:103-117
+ * (err(k) = v_k'(-A uh_k - M~ + F)), python/Main_finite_difference.py:79-94 (errEst, "the
+ * Adjoint-Weighted Residual as an error estimate": res[n] = u_f[n] - Phi(u_f[n-1]) of the
+ * interpolated state).  Here, for the linear LSERK4 advection sweep:
+ *   lo      the order-N plan of the forward sweep; hi an order-(N+1) plan on the same mesh
+ *           (same K, batch, vertices, a, inflow; linear flux, no limiter, LSERK4); N <= 7
+ *   P       host (N+2) x (N+1) row-major: u_hi = P u_lo, the interpolation of the element
+ *           polynomials to the order-(N+1) nodes (Vandermonde1D(N, r_hi) * invV_lo)
+ *   eta[e] (+)= - sum_{n=0}^{nsteps-1} w^{n+1}[e] . R^n[e],
+ *           R^n = P u^{n+1} - S_{N+1}(P u^n, t_n)   (the enriched scheme's one-step residual)
+ *           w^{n+1} = (S_{N+1}^T)^{nsteps-1-n} w    (the order-(N+1) discrete adjoint)
+ *   so that sum_e eta[e] = w . (u_{N+1}^nsteps - P u^nsteps) with u_{N+1} the order-(N+1)
+ *   march from P u^0: for a linear functional J with gradient w this is
+ *   J_{N+1}(u_{N+1}) - J_{N+1}(P u_h), the DWR identity (oracle/effectivity.py p_indicator).
+ *
+ * dg_prolong: u_hi = P u (device fields of the lo / hi plans' sizes).
+ * dg_lserk4_adj_p:
+ *   w (in/out, hi field): the terminal weight dJ_{N+1}/du on entry, w^0 on exit.
+ *   snapshots: the (nsteps+1) order-N states dg_lserk4_fwd wrote (snapshots[n] = u^n).
+ *   eta (nullable, batch*K) and flags as dg_lserk4_adj_ex (DG_ADJ_ETA_ASSIGN / _ABS).
+ * Scratch: the hi plan's.  Neither plan may be used concurrently. */
+int dg_prolong(const dg_plan* lo, const dg_plan* hi, const double* P, const double* u,
+               double* u_hi, void* stream);
+int dg_lserk4_adj_p(dg_plan* lo, dg_plan* hi, const double* P, double* w,
+                    const double* snapshots, double t0, double dt, int nsteps, double* eta,
+                    int flags, void* stream);
 
 /* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */

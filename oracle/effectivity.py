@@ -98,17 +98,30 @@ def jump_indicator(snaps, times, dt, a, S, inflow=INFLOW_ZERO):
   return eta
 
 
-def p_indicator(snaps, times, dt, a, S, S_hi, inflow=INFLOW_ZERO):
-  """The p-prolonged residual variant (order N+1 residual and adjoint), and the order-(N+1)
-  solution's functional for reference.  Returns (eta, J_{N+1}(u_{N+1}))."""
+def p_estimate(snaps, times, dt, a, S, S_hi, g_hi, inflow=INFLOW_ZERO):
+  """The p-prolonged residual estimate for the terminal weight g_hi (order N+1): the CPU
+  statement of dg_lserk4_adj_p (include/dg_advec.h).  Per step n (MAIN.m:32-34 marches the
+  adjoint at order Ns+1; adj_march.m:117 pairs it with the residual; errEst's
+  res[n] = u_f[n] - Phi(u_f[n-1]), Main_finite_difference.py:79-94):
+    R^n = P u^{n+1} - S_{N+1}(P u^n, t_n),   eta_k -= w^{n+1}_k . R^n_k.
+  Returns (eta, w^0) with w^0 the order-(N+1) adjoint at t_0."""
   P = prolong_matrix(S, S_hi)
   ps = [P @ u for u in snaps]
-  hi_snaps, _ = forward_sweep(ps[0], times[0], dt, len(snaps) - 1, a, S_hi, inflow)
-  ws = adjoint_weights(hi_snaps, weight(S_hi), dt, a, S_hi)
+  ws = adjoint_weights(ps, g_hi, dt, a, S_hi)  # the linear adjoint needs no states
   eta = np.zeros(S["K"])
   for n in range(len(snaps) - 1):
     R = ps[n + 1] - step(ps[n], times[n], dt, a, S_hi, inflow)
     eta -= np.sum(ws[n + 1] * R, axis=0)
+  return eta, ws[0]
+
+
+def p_indicator(snaps, times, dt, a, S, S_hi, inflow=INFLOW_ZERO):
+  """The p-prolonged residual variant (order N+1 residual and adjoint) for the window
+  functional, and the order-(N+1) solution's functional for reference.
+  Returns (eta, J_{N+1}(u_{N+1}))."""
+  P = prolong_matrix(S, S_hi)
+  hi_snaps, _ = forward_sweep(P @ snaps[0], times[0], dt, len(snaps) - 1, a, S_hi, inflow)
+  eta, _ = p_estimate(snaps, times, dt, a, S, S_hi, weight(S_hi), inflow)
   return eta, functional(hi_snaps[-1], S_hi)
 
 

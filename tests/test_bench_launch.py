@@ -86,3 +86,29 @@ def test_bench_accounting_helpers():
   assert abs(bench.eo_flops_per_update(5, True) - 57.4) < 1e-12
   for Np in range(2, 10):  # fewer flops than SURVEY 8d's dense count 5 (2 Np + 11)
     assert bench.eo_flops_per_update(Np, False) < 5 * (2 * Np + 11)
+
+
+def test_rank_device_binds_rccl_to_one_gpu_per_rank():
+  """init_dist's plan: RCCL ranks get their own GPU and the process group
+  is bound to it (device_id); more ranks than GPUs is refused with a clear message, not left
+  to RCCL; gloo shares GPUs round-robin (the one-GPU-box tests); one rank needs no group."""
+  b = _bench()
+  assert b.rank_device("nccl", 8, 3, 8, 8) == (3, {"backend": "nccl", "device_id": 3})
+  with pytest.raises(RuntimeError, match="one GPU per rank"):
+    b.rank_device("nccl", 2, 1, 2, 1)
+  assert b.rank_device("gloo", 2, 1, 2, 1) == (0, {"backend": "gloo"})
+  assert b.rank_device("nccl", 1, 0, 1, 1) == (0, None)
+  with pytest.raises(RuntimeError, match="needs a ROCm GPU"):
+    b.rank_device("nccl", 1, 0, 1, 0)
+
+
+def test_bench_p_indicator_accounting():
+  """--indicator p implies the snapshot forward; k_adj_p's flop count (prolongation +
+  order-(N+1) forward step + residual pairing + order-(N+1) reverse step per element-step)
+  exceeds the jump adjoint's, and the halo factor is T / (T - 2H)."""
+  b = _bench()
+  a = b.parse(["--indicator", "p"])
+  assert a.record == "snapshots" and a.indicator == "p"
+  for Np in range(2, 9):
+    assert b.p_flops_per_update(Np) > b.eo_flops_per_update(Np + 1, True)
+  assert b.halo_factor(1024, 50) == 1024 / 924.0

@@ -34,13 +34,37 @@ def test_bench_single_rank_line(gpu):
   assert out["nonfinite_indicator_steps"] == 0
   assert out["stream_copy"]["achievable_GBs"] > 1000
   assert out["refine_index_ranks"] == [out["refine_index"]]
+  assert "flops" not in out and out["dist_world_size"] == 1 and out["collective_backend"] is None
+  fp = out["roofline_fp64"]
+  for key in ("adj_frac", "fwd_frac", "adj_issued_frac", "fwd_issued_frac"):
+    assert 0 < fp[key] <= 1, key
+  assert fp["adj_issued_frac"] >= fp["adj_frac"] and fp["fwd_halo_factor"] > 1
+  assert out["indicator"] == "jump" and "resolved" in out["indicator_resolved"]
+  assert out["library"]["path"].endswith("libdgadv.so") and not out["library"]["override"]
+
+
+def test_bench_p_estimate_line(gpu):
+  """--indicator p: the forward keeps snapshots, the adjoint is k_adj_p (order N+1 + the
+  prolonged one-step residual); its line carries the same roofline blocks and a CPU baseline
+  of the oracle's p-estimate."""
+  out = _run(["--K", "65536", "--steps", "3", "--warmup", "2", "--no-converge",
+              "--cpu-steps", "2"])
+  assert out["indicator"] == "jump"
+  out = _run(["--K", "65536", "--steps", "3", "--warmup", "2", "--no-converge",
+              "--indicator", "p", "--cpu-steps", "2"])
+  assert out["indicator"] == "p" and out["config"]["record"] == "snapshots"
+  assert out["roofline"]["kernel"].startswith("k_adj_p<5")
+  assert 0 < out["roofline"]["frac"] < 1 and out["prolong_us"] > 0
+  assert out["nonfinite_indicator_steps"] == 0
+  assert out["cpu_baseline"]["value"] > 0 and "p-enriched" in out["cpu_baseline"]["sample"]
 
 
 @pytest.mark.parametrize("extra", [[], ["--ics", "6"]])
 def test_bench_self_launches_two_ranks(gpu, extra):
   out = _run(["--gpus", "2", "--backend", "gloo", "--K", "65536", "--steps", "2",
               "--warmup", "1", "--no-converge", "--no-cpu-baseline", *extra])
-  assert out["n_gpus"] == 2 and out["rccl_world_size"] == 2
+  assert out["n_gpus"] == 2 and out["dist_world_size"] == 2
+  assert out["collective_backend"] == "gloo"  # never reported as RCCL when gloo ran
   ranks = out["refine_index_ranks"]
   assert len(ranks) == 2 and ranks[0] == ranks[1] == out["refine_index"]
   if extra:

@@ -343,3 +343,48 @@ def test_forward_own_steps_per_launch(pkg, gpu):
   del big
   mid = pkg.operators.DGAdvection1D(pkg.BaseGalerkin1D(n=4, k=1 << 20), batch=3)
   assert mid.rec_fwd_steps_per_launch == 20
+
+
+def test_adjoint_rec_needs_the_record_even_without_eta(pkg, gpu):
+  """The record kernels read the record on every reverse step, so a null record is an
+  argument error whenever there is a step to run, also with eta = NULL; with
+  the record and eta = NULL, w is the eta run's w bit for bit."""
+  import ctypes
+
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=4, k=300)
+  op = pkg.operators.DGAdvection1D(mesh)
+  dt = mesh.cfl_dt()
+  u0 = torch.sin(torch.linspace(0, 6.0, op.field_numel, dtype=torch.float64, device=gpu))
+  rec = op.new_jumps(5)
+  uN = op.new_field()
+  op.forward_rec(u0, 0.0, dt, 5, rec, out=uN)
+  w = uN.clone()
+  rc = op._lib.dg_lserk4_adj_rec(op._plan, ctypes.c_void_p(w.data_ptr()), None, 0.0, dt, 5,
+                                 None, 0, None)
+  assert rc == pkg._lib.DG_ERR_ARG and b"null" in op._lib.dg_last_error()
+  assert torch.equal(w, uN)  # refused before any launch
+  w_noeta, w_eta = uN.clone(), uN.clone()
+  op.adjoint_rec(w_noeta, rec, 0.0, dt, 5)
+  eta = torch.zeros(op.ktot, dtype=torch.float64, device=gpu)
+  op.adjoint_rec(w_eta, rec, 0.0, dt, 5, eta=eta)
+  torch.cuda.synchronize()
+  assert torch.equal(w_noeta, w_eta)
+  # nsteps = 0: nothing to read, a null record is fine
+  assert op._lib.dg_lserk4_adj_rec(op._plan, ctypes.c_void_p(w.data_ptr()), None, 0.0, dt, 0,
+                                   None, 0, None) == 0
+
+
+def test_env_override_is_the_tune_key(pkg, gpu, monkeypatch):
+  """DG_REC_STEPS_PER_LAUNCH sets the record steps per launch of both directions, as
+  dg_plan_tune(DG_TUNE_REC_STEPS_PER_LAUNCH) does (the env override used to leave
+  the forward on its size-based 20-step default)."""
+  mesh = pkg.BaseGalerkin1D(n=4, k=2000)
+  tuned = pkg.operators.DGAdvection1D(mesh).tune(rec_steps_per_launch=8)
+  monkeypatch.setenv("DG_REC_STEPS_PER_LAUNCH", "8")
+  env = pkg.operators.DGAdvection1D(mesh)
+  assert (env.rec_steps_per_launch, env.rec_fwd_steps_per_launch) == \
+      (tuned.rec_steps_per_launch, tuned.rec_fwd_steps_per_launch) == (8, 8)
+  monkeypatch.setenv("DG_REC_FWD_STEPS_PER_LAUNCH", "20")  # the forward's own override wins
+  both = pkg.operators.DGAdvection1D(mesh)
+  assert (both.rec_steps_per_launch, both.rec_fwd_steps_per_launch) == (8, 20)

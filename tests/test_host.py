@@ -183,3 +183,18 @@ def test_check_indicator_flags_non_finite(pkg):
   for bad in (math.nan, math.inf, -math.inf):
     with pytest.raises(FloatingPointError):
       pkg.adaptive.check_indicator(bad, 3)
+
+
+def test_prolongation_is_the_oracles_interpolation(pkg):
+  """galerkin.prolongation (the P handed to dg_lserk4_adj_p) = oracle.effectivity's
+  prolong_matrix, and it reproduces degree-N polynomials at the order-(N+1) nodes."""
+  import numpy as np
+  from oracle import effectivity as ef
+  from oracle import setup1d
+  for N in range(1, 8):
+    vx = np.linspace(0.0, 1.0, 5)
+    lo, hi = pkg.BaseGalerkin1D(n=N, v_x=vx), pkg.BaseGalerkin1D(n=N + 1, v_x=vx)
+    P = pkg.galerkin.prolongation(lo, hi)
+    Po = ef.prolong_matrix(setup1d.startup1d(N, vx), setup1d.startup1d(N + 1, vx))
+    assert np.max(np.abs(P - Po)) <= 1e-13
+    assert np.max(np.abs(P @ lo.r_gl ** N - hi.r_gl ** N)) <= 1e-13
