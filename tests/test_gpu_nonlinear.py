@@ -339,3 +339,75 @@ def test_diverged_sweep_is_refused(pkg, gpu):
   run = pkg.adaptive.AdaptiveSweep(mesh, 300, 2, flux="linear", limiter=False, cfl=60.0)
   with pytest.raises(FloatingPointError):
     run.iterate()
+
+
+def window_setup(N, v_x, k0, k1, s_glob):
+  """The oracle's setup on elements [k0, k1) of a uniform mesh, with the plan's global
+  metric 2/mean(h) (the window's own mean differs in the last bit)."""
+  S = setup1d.startup1d(N, v_x[k0:k1 + 1], metric="element")
+  S["rx"][:] = s_glob
+  S["Fscale"][:] = s_glob
+  S["J"][:] = 1.0 / s_glob
+  return S
+
+
+@pytest.mark.slow
+def test_full_size_config3_adjoint_and_indicator(pkg, gpu):
+  """BASELINE config 3 size (N=4, K=4,194,304, Burgers + SlopeLimitN per stage, 2 steps):
+  the GPU's adjoint w^0 and indicator eta against oracle/burgers.py's adjoint sweep on the
+  GPU's own snapshots.  The oracle's coloured-Jacobian transpose costs
+  ~100 tangent sweeps per step, so it runs on windows of the full mesh: w^0 and eta of an
+  element depend only on the snapshots and w^N within the adjoint's cone (10 elements per
+  limited step and side), so on a window's interior -- 30 elements in from a cut -- the
+  windowed oracle is the full-size oracle.  Windows: the inflow boundary, the jump at x = 0.5
+  (troubled cells), a random interior stretch and the outflow boundary."""
+  import torch
+  N, K, nsteps, margin = 4, 1 << 22, 2, 30
+  _, v_x, _, _ = setup1d.mesh_gen1d(0.0, 1.0, K)
+  mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+  op = pkg.operators.DGAdvection1D(mesh, flux="burgers", limiter=True)
+  assert op.uniform
+  h = np.diff(v_x)
+  s_glob = 2.0 / (np.cumsum(h)[-1] / K)
+  rng = np.random.default_rng(42)
+  snaps = op.new_field(nsteps + 1)
+  # u0 = sin(2 pi x) + 0.8 (x > 0.5) + seeded per-node noise, built on the device from the
+  # node coordinates.  The noise makes the interelement jumps O(0.01) everywhere: a smooth
+  # IC's jumps at h = 2^-22 are below fp64 resolution, its indicator rounding noise (the
+  # first version of this test saw |eta| ~ 1e-16 in the interior window).
+  r = torch.tensor(setup1d.jacobi_gl(0, 0, N), dtype=torch.float64, device=gpu)
+  vxd = torch.tensor(v_x, dtype=torch.float64, device=gpu)
+  xd = vxd[:-1, None] + 0.5 * (r[None, :] + 1.0) * (vxd[1:] - vxd[:-1])[:, None]  # (K, Np)
+  gen = torch.Generator(device=gpu).manual_seed(7)
+  noise = torch.randn(xd.shape, generator=gen, dtype=torch.float64, device=gpu)
+  snaps[0].copy_((torch.sin(2 * np.pi * xd) + 0.8 * (xd > 0.5) + 0.01 * noise).reshape(-1))
+  dt = mesh.cfl_dt()
+  op.forward(snaps[0], 0.0, dt, nsteps, snaps)
+  wT = (torch.cos(3 * np.pi * xd) + 0.2 * torch.sin(11 * np.pi * xd)).reshape(-1)
+  w = wT.clone()
+  eta = torch.zeros(K, dtype=torch.float64, device=gpu)
+  op.adjoint(w, snaps, 0.0, dt, nsteps, eta=eta)
+  torch.cuda.synchronize()
+  times = [0.0]
+  for _ in range(nsteps):
+    times.append(times[-1] + dt)
+  k_jump = int(np.searchsorted(v_x, 0.5)) - 200
+  k_rand = int(rng.integers(1000, K - 2000))
+  Np = N + 1
+  for k0, k1 in ((0, 400), (k_jump, k_jump + 400), (k_rand, k_rand + 400), (K - 400, K)):
+    S = window_setup(N, v_x, k0, k1, s_glob)
+    sl = slice(k0 * Np, k1 * Np)
+    gs = [setup1d.from_elem_major(host(snaps[n][sl]), Np) for n in range(nsteps + 1)]
+    gw = setup1d.from_elem_major(host(wT[sl]), Np)
+    w_ref, eta_ref, _ = ob.adjoint_sweep(gw, gs, times, dt, A, S, limit=True)
+    lo = 0 if k0 == 0 else margin  # a real boundary needs no margin
+    hi = (k1 - k0) if k1 == K else (k1 - k0) - margin
+    got_w = setup1d.from_elem_major(host(w[sl]), Np)[:, lo:hi]
+    assert rel_err(got_w, w_ref[:, lo:hi]) <= RTOL, (k0, rel_err(got_w, w_ref[:, lo:hi]))
+    got_eta = host(eta[k0:k1])[lo:hi]
+    assert rel_err(got_eta, eta_ref[lo:hi]) <= RTOL, (k0, rel_err(got_eta, eta_ref[lo:hi]))
+  # the jump window holds troubled cells (the frozen-decision transpose is exercised)
+  u_mid = setup1d.from_elem_major(host(snaps[1][k_jump * Np:(k_jump + 400) * Np]), Np)
+  _, ids = ob.limited_step(u_mid, times[1], dt, A, window_setup(N, v_x, k_jump, k_jump + 400,
+                                                                  s_glob), return_ids=True)
+  assert sum(i.size for i in ids) > 0
