@@ -22,6 +22,7 @@ DG_TUNE_LANE_ELEMENTS = 4
 DG_TUNE_REC_TILE_WIDTH, DG_TUNE_REC_STEPS_PER_LAUNCH = 5, 6
 DG_TUNE_REC_LANE_ELEMENTS, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 7, 8
 DG_TUNE_P_TILE_WIDTH, DG_TUNE_P_STEPS_PER_LAUNCH = 9, 10
+DG_TUNE_REC_FWD_TILE_WIDTH = 11
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
@@ -53,6 +54,7 @@ SIGNATURES = {
     "dg_lserk4_fwd_ex": (_i32, [_vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp, _vp,
                                 _vp]),
     "dg_plan_query_rec": (_i32, [_vp, _vp]),
+    "dg_plan_query_rec_fwd": (_i32, [_vp, _vp]),
     "dg_lserk4_fwd_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,
                                  _vp]),
     "dg_lserk4_adj_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,

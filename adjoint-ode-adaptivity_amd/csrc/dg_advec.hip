@@ -45,14 +45,13 @@ __global__ __launch_bounds__(kBlock * W) void k_adj(const double* __restrict__ w
                                                     const double* __restrict__ scale,
                                                     AdjArgs<NP, MS> args);
 
-// The jump record (dg_lserk4_fwd_rec / dg_lserk4_adj_rec).  The indicator needs of u^n only
-// the two interelement jumps of each element, du0 = u_0 - uL and du1 = u_N - uR (the DWR
-// residual R(u^n) = LIFT Fscale du, utils/AdvecRHS1D.m:19): the forward records, per element
-// and step, (du0 - du1, du0 + du1) -- 16 bytes where a snapshot takes 8 Np -- computed from
-// the face values its stage 0 exchanges anyway, with exactly the adjoint's arithmetic, so
-// eta is bit-identical to the snapshot sweep's.  Record n-1 holds u^n's jumps, n = 1..nsteps.
-__device__ __forceinline__ double2* jump_slot(double* rec, int64_t n, int64_t ktot, int64_t e) {
-  return reinterpret_cast<double2*>(rec) + (n * ktot + e);
+// The jump record (dg_lserk4_fwd_rec / dg_lserk4_adj_rec; layout in dg_common.h rec_ld): per
+// element and step the left-face jump j_e = u_0 - uL -- 8 bytes where a snapshot takes 8 Np --
+// computed from the face values stage 0 exchanges anyway; the adjoint rebuilds
+// du0 - du1 = j_e + j_{e+1} and du0 + du1 = j_e - j_{e+1} (du1 = 0 at a trajectory's last
+// element), the snapshot path's doubles, so eta is bit-identical to the snapshot sweep's.
+__device__ __forceinline__ double* jump_row(double* rec, int64_t n, int64_t ktot) {
+  return rec + n * rec_ld(ktot);
 }
 
 // ---------------------------------------------------------------------------
@@ -114,9 +113,7 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
       if (args.n0 >= 1 && E[m].valid) {
         const double* us = lds + pf.off + el * NP;
         const double uL = (EDGE && E[m].first) ? lds[CB] : us[-1];
-        const double uR = (EDGE && E[m].last) ? us[NP - 1] : us[NP];
-        const double du0 = us[0] - uL, du1 = us[NP - 1] - uR;
-        *jump_slot(snap, args.n0 - 1, args.ktot, E[m].e) = double2{du0 - du1, du0 + du1};
+        jump_row(snap, args.n0 - 1, args.ktot)[E[m].e] = us[0] - uL;
       }
     }
   }
@@ -180,10 +177,8 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
         const double uL = lds[iL], uR = lds[iR];
         const double dlt = uR - uL, sig = -(uL + uR);
         if constexpr (REC) {  // u^{n0+st}'s jumps (record n0+st-1), stage 0 of its step
-          if (s == 0 && st >= 1 && E[m].valid) {
-            const double du0 = u0[m] - uL, du1 = uN[m] - uR;
-            *jump_slot(snap, args.n0 + st - 1, args.ktot, E[m].e) = double2{du0 - du1, du0 + du1};
-          }
+          if (s == 0 && st >= 1 && E[m].valid)
+            jump_row(snap, args.n0 + st - 1, args.ktot)[E[m].e] = u0[m] - uL;
         }
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
@@ -217,11 +212,7 @@ __device__ __forceinline__ void step_tile(double* __restrict__ lds, int64_t tile
       lds[fR + el + 1] = uN;
       __syncthreads();
       const int iL = EDGE && E[0].first ? CB + MS * NS : fR + el;
-      const int iR = EDGE && E[0].last ? fR + el + 1 : fL + el + 2;
-      if (E[0].valid) {
-        const double du0 = u0 - lds[iL], du1 = uN - lds[iR];
-        *jump_slot(snap, args.n0 + MS - 1, args.ktot, E[0].e) = double2{du0 - du1, du0 + du1};
-      }
+      if (E[0].valid) jump_row(snap, args.n0 + MS - 1, args.ktot)[E[0].e] = u0 - lds[iL];
     }
     if ((!REC && snap != nullptr) || st == MS - 1) {
       // The image's last readers (staging reads, the previous step's store) are at least
@@ -286,13 +277,16 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
 
   constexpr int CB = G::kLds;  // lds[CB + st] = inflow value at t_{n+st+1}; lds[CB + MS] = 0
   TileRegs<NP, W> pw, pu;
-  // REC: the jumps of u^{n0+st+1} (record n0+st), one 16-byte load per lane and step,
-  // prefetched a step ahead
+  // REC: the left-face jumps of u^{n0+st+1} (record n0+st) of the lane's element and of its
+  // right neighbour, two 8-byte loads per lane and step, prefetched a step ahead
   const bool jin = REC && e0 + lane >= 0 && e0 + lane < args.ktot;
-  double2 jn{0.0, 0.0};
+  const bool jin1 = REC && e0 + lane + 1 >= 0 && e0 + lane + 1 < args.ktot;
+  double jn = 0.0, jn1 = 0.0;
   tile_issue<NP, W, EDGE>(win, e0, nd, pw);
   if constexpr (REC) {
-    if (jin) jn = *jump_slot(const_cast<double*>(snap), args.n0 + MS - 1, args.ktot, e0 + lane);
+    const double* row = jump_row(const_cast<double*>(snap), args.n0 + MS - 1, args.ktot);
+    if (jin) jn = row[e0 + lane];
+    if (jin1) jn1 = row[e0 + lane + 1];
   } else {
     tile_issue<NP, W, EDGE>(snap + (MS - 1) * args.stride, e0, nd, pu);
   }
@@ -333,16 +327,21 @@ __device__ __forceinline__ void adj_tile(double* __restrict__ lds, int64_t tile,
   for (int st = MS - 1; st >= 0; --st) {
     if constexpr (REC) {
       // no snapshot: the record's jumps replace the staged tile's neighbour faces
-      const double2 jc = jn;
-      if (st > 0 && jin)
-        jn = *jump_slot(const_cast<double*>(snap), args.n0 + st - 1, args.ktot, e0 + lane);
+      const double jc = jn, jc1 = jn1;
+      if (st > 0) {
+        const double* row = jump_row(const_cast<double*>(snap), args.n0 + st - 1, args.ktot);
+        if (jin) jn = row[e0 + lane];
+        if (jin1) jn1 = row[e0 + lane + 1];
+      }
       if (args.has_eta) {
         double pe = 0.0, po = 0.0;
 #pragma unroll
         for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[0][k], pe);
 #pragma unroll
         for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[0][k], po);
-        double c = fma(jc.x, pe, jc.y * po);
+        // du0 = j_e, du1 = -j_{e+1} (0 at a trajectory's last element)
+        const bool lst = EDGE && E[0].last;
+        double c = fma(lst ? jc : jc + jc1, pe, (lst ? jc : jc - jc1) * po);
         if constexpr (!UNI) c *= sc[0];
         eacc[0] += c;
       }
@@ -830,7 +829,7 @@ template <int NP> LimArgs<NP> make_lim(const dg_plan* p) {
   return la;
 }
 
-// Jump-record sweeps (REC): `snap` is the record, `rec` = {n0, jend} (see jump_slot).
+// Jump-record sweeps (REC): `snap` is the record, `rec` = {n0, jend} (see jump_row).
 struct RecPos {
   int64_t n0 = 0;
   bool jend = false;
@@ -959,10 +958,11 @@ int launch_adj(const dg_plan* p, int ms, const double* win, double* wout, const 
   return rc;
 }
 
-// Record sweeps run on pair tiles (dg_rec.hip) for Np <= 8.  The one-element-per-lane record
-// kernels below: W = 1 with 1..4 steps, W = 2 with 1..8; Np = 9: at most 2 steps (1024-element
-// one-element-per-lane tiles -- 16-wave workgroups, 74 KB of LDS -- measured 20 % slower).
-inline bool rec_pairs(const dg_plan* p) { return p->rec_lane_elems == 2 && p->NP <= 8; }
+// Record sweeps run on pair tiles (dg_rec.hip), Np <= 9, unless DG_TUNE_REC_LANE_ELEMENTS = 1
+// selects the one-element-per-lane record kernels below: W = 1 with 1..4 steps, W = 2 with
+// 1..8; Np = 9: at most 2 steps there (1024-element one-element-per-lane tiles -- 16-wave
+// workgroups, 74 KB of LDS -- measured 20 % slower).
+inline bool rec_pairs(const dg_plan* p) { return p->rec_lane_elems == 2; }
 
 // Record steps per launch: pair tiles take 1, 2, 4, 5, 8, 10, 16 or 20 (a sweep is chunked by
 // halving: 20 -> 10 -> 5 -> 2 -> 1); the one-element-per-lane kernels 1, 2, 4 or 8.
@@ -970,21 +970,22 @@ inline bool rec_msteps_ok(int k) {
   return k == 1 || k == 2 || k == 4 || k == 5 || k == 8 || k == 10 || k == 16 || k == 20;
 }
 
-// The record steps per launch the plan's shape allows for a requested value m.
-inline int rec_msteps_cap(const dg_plan* p, int m) {
+// The record steps per launch the plan's shape allows for a requested value m on tiles of
+// width w.
+inline int rec_msteps_cap(const dg_plan* p, int m, int w) {
   if (!rec_pairs(p)) {
     int q = 1;
     while (q * 2 <= m && q < 8) q *= 2;
     m = q;
   }
-  if (m == 8 && p->rec_tile_width == 1 && !rec_pairs(p)) m = 4;
-  if (rec_pairs(p) && p->rec_tile_width == 1 && m > 10) m = (m == 16) ? 8 : 10;
-  if (p->NP > 8 && m > 2) m = 2;
+  if (m == 8 && w == 1 && !rec_pairs(p)) m = 4;
+  if (rec_pairs(p) && w == 1 && m > 10) m = (m == 16) ? 8 : 10;
+  if (!rec_pairs(p) && p->NP > 8 && m > 2) m = 2;
   return m;
 }
 
 // Adjoint (and, unless overridden, forward) record steps per launch.
-inline int rec_msteps(const dg_plan* p) { return rec_msteps_cap(p, p->rec_msteps); }
+inline int rec_msteps(const dg_plan* p) { return rec_msteps_cap(p, p->rec_msteps, p->rec_tile_width); }
 
 // Forward record steps per launch.  By size (the default): one 20-step launch on 1024-element
 // pair tiles while a 10-step launch would be only ~1.5-4 rounds of workgroups (up to 3*2^20
@@ -994,12 +995,10 @@ inline int rec_msteps(const dg_plan* p) { return rec_msteps_cap(p, p->rec_msteps
 inline int rec_msteps_fwd(const dg_plan* p) {
   int m = p->rec_msteps_fwd;
   if (m < 0)
-    m = (rec_pairs(p) && p->rec_tile_width == 2 && p->ktot <= (int64_t(3) << 20)) ? 20
-                                                                               : p->rec_msteps;
-  return rec_msteps_cap(p, m ? m : p->rec_msteps);
+    m = (rec_pairs(p) && rec_fwd_width(p) == 2 && p->ktot <= (int64_t(3) << 20)) ? 20
+                                                                             : p->rec_msteps;
+  return rec_msteps_cap(p, m ? m : p->rec_msteps, rec_fwd_width(p));
 }
-
-inline int rec_width(const dg_plan* p, int /*ms*/) { return p->rec_tile_width; }
 
 // Jump-record launches: LSERK4 (NS = 5) on the workgroup tiles, the plan's tile width and
 // steps per launch (the 8-step shape on 512-element tiles; Np = 9 at most 2 steps).
@@ -1008,8 +1007,7 @@ int launch_step_rec_t(const dg_plan* p, int ms, const double* in, double* rec, d
                       const double* times, double dt, hipStream_t st, RecPos pos) {
   if (rec_pairs(p))
     return pair_launch_step_rec(p, ms, in, rec, last, times, dt, st, pos.n0, pos.jend);
-  const int w = rec_width(p, ms);
-  const bool w2 = w == 2;
+  const bool w2 = rec_fwd_width(p) == 2;
   if constexpr (NP <= 8) {
     if (ms == 8) return launch_step_e<NP, 5, 2, 8, true>(p, in, rec, last, times, dt, st, pos);
     if (ms == 4 && w2) return launch_step_e<NP, 5, 2, 4, true>(p, in, rec, last, times, dt, st, pos);
@@ -1027,8 +1025,7 @@ int launch_adj_rec_t(const dg_plan* p, int ms, const double* win, double* wout, 
                      hipStream_t st, int64_t n0) {
   if (rec_pairs(p))
     return pair_launch_adj_rec(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
-  const int w = rec_width(p, ms);
-  const bool w2 = w == 2;
+  const bool w2 = p->rec_tile_width == 2;
   if constexpr (NP <= 8) {
     if (ms == 8)
       return launch_adj_e<NP, 5, 2, 8, true>(p, win, wout, rec, eta, em, t_next, src, dt, st, n0);
@@ -1148,8 +1145,15 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   // leave a 4-step launch in a 20-step sweep.)
   p->tile_width = (N <= 2) ? 2 : 1;
   if (N <= 2) p->lane_elems = 4;
-  // Record sweeps: pair tiles (2 elements per lane, dg_rec.hip) for Np <= 8; at Np = 9 the
-  // one-element-per-lane kernels on 512-element tiles, 2 steps (rec_msteps caps it).
+  // Record sweeps: pair tiles (2 elements per lane, dg_rec.hip) at every Np.  At Np = 9 the
+  // adjoint (147 VGPRs: 3 waves per SIMD) runs 512-element tiles -- three 4-wave workgroups
+  // fill a CU where one 8-wave workgroup leaves a third of the wave slots empty -- and the
+  // forward (122 VGPRs) keeps 1024-element tiles and its one 20-step launch: 330 + 395 us per
+  // 20-step sweep at K = 2^20 against 336 + 477 with both on 1024 (profiles/r03/perN/ab_N8.json).
+  if (p->NP == 9) {
+    p->rec_tile_width = 1;
+    p->rec_tile_width_fwd = 2;
+  }
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);
@@ -1165,7 +1169,14 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     }
     if (const char* v = std::getenv("DG_REC_TILE_WIDTH")) {
       const int k = std::atoi(v);
-      if (k == 1 || k == 2) p->rec_tile_width = k;
+      if (k == 1 || k == 2) {
+        p->rec_tile_width = k;
+        p->rec_tile_width_fwd = 0;  // both directions, as DG_TUNE_REC_TILE_WIDTH
+      }
+    }
+    if (const char* v = std::getenv("DG_REC_FWD_TILE_WIDTH")) {
+      const int k = std::atoi(v);
+      if (k == 0 || k == 1 || k == 2) p->rec_tile_width_fwd = k;
     }
     if (const char* v = std::getenv("DG_REC_STEPS_PER_LAUNCH")) {
       const int k = std::atoi(v);
@@ -1241,10 +1252,17 @@ int dg_plan_query(const dg_plan* p, int64_t out[8]) {
 int dg_plan_query_rec(const dg_plan* p, int64_t out[4]) {
   if (!p || !out) return fail(DG_ERR_ARG, "null argument");
   const int m = rec_msteps(p);
-  out[0] = rec_width(p, m);
+  out[0] = p->rec_tile_width;
   out[1] = m;
   out[2] = rec_pairs(p) ? 2 : 1;
   out[3] = rec_msteps_fwd(p);
+  return DG_OK;
+}
+
+int dg_plan_query_rec_fwd(const dg_plan* p, int64_t out[2]) {
+  if (!p || !out) return fail(DG_ERR_ARG, "null argument");
+  out[0] = rec_fwd_width(p);
+  out[1] = rec_msteps_fwd(p);
   return DG_OK;
 }
 
@@ -1271,6 +1289,12 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       if (value != 1 && value != 2)
         return fail(DG_ERR_ARG, "record tile width must be 1 or 2");
       p->rec_tile_width = int(value);
+      p->rec_tile_width_fwd = 0;  // both directions
+      return DG_OK;
+    case DG_TUNE_REC_FWD_TILE_WIDTH:
+      if (value != 0 && value != 1 && value != 2)
+        return fail(DG_ERR_ARG, "forward record tile width must be 0 (as the adjoint's), 1 or 2");
+      p->rec_tile_width_fwd = int(value);
       return DG_OK;
     case DG_TUNE_REC_STEPS_PER_LAUNCH:
       if (!rec_msteps_ok(int(value)))

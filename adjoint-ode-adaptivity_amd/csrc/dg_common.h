@@ -47,6 +47,17 @@ __device__ __forceinline__ void eta_update(double* __restrict__ eta, int64_t e, 
   eta[e] = v;
 }
 
+// The jump record (dg_lserk4_fwd_rec / dg_lserk4_adj_rec).  The indicator needs of u^n only
+// the interelement jumps (utils/AdvecRHS1D.m:9-16's du; R(u^n) = LIFT Fscale du, :19), and a
+// face's jump is one number shared by its two elements: the record keeps, per step and
+// element e, the LEFT-face jump j_e = u_0 - uL (uL = the inflow value at a trajectory's first
+// element), one double.  Element e's right-face jump du1 = u_N - uR is -j_{e+1} exactly
+// (IEEE subtraction is antisymmetric: b - a == -(a - b)), or 0 at a trajectory's last element,
+// so the adjoint rebuilds du0 - du1 = j_e + j_{e+1} and du0 + du1 = j_e - j_{e+1} bit for bit.
+// Row n - 1 holds u^n's jumps; rows are rec_ld(ktot) doubles apart (ktot rounded up to even,
+// so the pair kernels' two-element accesses are 16-byte aligned).
+__host__ __device__ constexpr int64_t rec_ld(int64_t ktot) { return (ktot + 1) & ~int64_t(1); }
+
 // Kernel-argument layout pin for the edge tiles' lane-indexed kernarg reads.  A kernel whose
 // parameters are pointers followed by ONE trailing by-value argument struct A has A at byte
 // offset (#pointers)*8 of the kernarg segment: pointers are 8-byte aligned and A's alignment
@@ -425,11 +436,12 @@ struct dg_plan {
   // defaults measured at N = 4, K = 2^20: 1024-element pair tiles, 10 steps per
   // launch (a 20-step sweep is 10 + 10 launches)
   int rec_tile_width = 2;
+  int rec_tile_width_fwd = 0;  // the forward record sweep's own tile width (0: as rec_tile_width)
   int rec_msteps = 10;
   // the forward's own record steps per launch: -1 by size (20 on 1024-element pair tiles up to
   // 3*2^20 elements, else as rec_msteps), 0 as rec_msteps, > 0 explicit
   int rec_msteps_fwd = -1;
-  int rec_lane_elems = 2;  // 2: the pair tiles of dg_rec.hip (Np <= 8), 1: dg_advec.hip k_step/k_adj
+  int rec_lane_elems = 2;  // 2: the pair tiles of dg_rec.hip, 1: dg_advec.hip k_step/k_adj
   // the p-enriched estimate's shape (dg_lserk4_adj_p, dg_dwr.hip): tile width 1 or 2 (256 or
   // 512 elements), steps per launch 1, 2, 4 or 8 (8 on 512-element tiles)
   int p_tile_width = 2;
@@ -443,6 +455,11 @@ struct dg_plan {
 };
 
 namespace dgk {
+
+// Tile width of the forward record sweep (the adjoint's is rec_tile_width).
+inline int rec_fwd_width(const dg_plan* p) {
+  return p->rec_tile_width_fwd ? p->rec_tile_width_fwd : p->rec_tile_width;
+}
 
 inline double inflow_value(const dg_plan* p, double t) {
   if (p->inflow == DG_INFLOW_ZERO) return 0.0;

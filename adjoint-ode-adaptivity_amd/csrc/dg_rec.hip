@@ -26,8 +26,8 @@
 namespace {
 using namespace dgk;
 
-template <int NP, int W, int E> struct RpGeo {
-  static constexpr int LB = kBlock * W;  // lanes per workgroup
+template <int NP, int NW, int E> struct RpGeo {
+  static constexpr int LB = 64 * NW;  // lanes per workgroup
   static constexpr int T = E * LB;       // elements per tile (incl. halo)
   static constexpr int kTileD = T * NP + 2;  // staging image (+2: 16-byte realignment)
   static constexpr int kVec = (kTileD + 2 * LB - 1) / (2 * LB);  // double2 loads per lane
@@ -37,10 +37,10 @@ template <int NP, int W, int E> struct RpGeo {
 
 // Coalesced 16-byte loads of the tile image [e0, e0 + T) (zeros outside [0, nd)), issued
 // together, then written to LDS.  Returns the image's offset (0 or 1 double).
-template <int NP, int W, int E, bool EDGE>
+template <int NP, int NW, int E, bool EDGE>
 __device__ __forceinline__ int rp_load(const double* __restrict__ g, int64_t e0, int64_t nd,
                                        double* __restrict__ lds) {
-  using G = RpGeo<NP, W, E>;
+  using G = RpGeo<NP, NW, E>;
   const int64_t d0 = e0 * NP;
   const int64_t base = d0 & ~int64_t(1);
   const int off = int(d0 - base);
@@ -72,12 +72,12 @@ __device__ __forceinline__ int rp_load(const double* __restrict__ g, int64_t e0,
 
 // The TE interior elements from registers to the image (nodal; `dual`: from the adjoint's
 // dual coordinates), then 16-byte stores.  Callers barrier before (face reads done).
-template <int NP, int W, int E, int H, bool EDGE>
+template <int NP, int NW, int E, int H, bool EDGE>
 __device__ __forceinline__ void rp_store(double* __restrict__ g, int64_t o0, int64_t nd,
                                          double* __restrict__ lds,
                                          const double (*ev)[(NP + 1) / 2],
                                          const double (*od)[NP / 2], bool dual) {
-  using G = RpGeo<NP, W, E>;
+  using G = RpGeo<NP, NW, E>;
   constexpr int T = G::T, TE = T - 2 * H;
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   const int lane = threadIdx.x;
@@ -107,12 +107,47 @@ __device__ __forceinline__ void rp_store(double* __restrict__ g, int64_t o0, int
   }
 }
 
-__device__ __forceinline__ double2* rp_slot(double* rec, int64_t n, int64_t ktot, int64_t e) {
-  return reinterpret_cast<double2*>(rec) + (n * ktot + e);  // = dg_advec.hip jump_slot
+// Halo widths (elements per side): the forward's stage cone MS*5 + the final state's
+// neighbours, the adjoint's MS*5; both rounded up to even, so every lane's element pair starts
+// at an even element and its two record entries are one aligned 16-byte access.
+template <int MS> struct RpHalo {
+  static constexpr int F = (MS * 5 + 2) & ~1;
+  static constexpr int A = (MS * 5 + 1) & ~1;
+};
+
+// Record row n: the lane's two left-face jumps (dg_common.h rec_ld), one 16-byte store; an
+// edge tile stores them one by one where its valid range ends between them.
+template <bool EDGE>
+__device__ __forceinline__ void rp_rec_put(double* __restrict__ rec, int64_t n, int64_t ktot,
+                                           const Elem* El, double j0, double j1) {
+  double* row = rec + n * rec_ld(ktot);
+  if (!EDGE || (El[0].valid && El[1].valid)) {
+    if (El[0].valid) *reinterpret_cast<double2*>(row + El[0].e) = double2{j0, j1};
+  } else {
+    if (El[0].valid) row[El[0].e] = j0;
+    if (El[1].valid) row[El[1].e] = j1;
+  }
 }
 
-template <int NP, bool UNI, int W, int E, int MS>
-__global__ __launch_bounds__(kBlock * W) void k_step_rp(const double* __restrict__ uin,
+// Record row n for the lane's pair starting at element ea (even): j_ea, j_ea+1 and the right
+// neighbour's j_ea+2.  Interior tiles never reach a trajectory's end, so all three are in
+// range; edge tiles read zeros outside [0, ktot).
+template <bool EDGE>
+__device__ __forceinline__ void rp_rec_get(const double* __restrict__ rec, int64_t n,
+                                           int64_t ktot, int64_t ea, double2& j01, double& j2) {
+  const double* row = rec + n * rec_ld(ktot);
+  if constexpr (!EDGE) {
+    j01 = *reinterpret_cast<const double2*>(row + ea);
+    j2 = row[ea + 2];
+  } else {
+    j01.x = (ea >= 0 && ea < ktot) ? row[ea] : 0.0;
+    j01.y = (ea + 1 >= 0 && ea + 1 < ktot) ? row[ea + 1] : 0.0;
+    j2 = (ea + 2 >= 0 && ea + 2 < ktot) ? row[ea + 2] : 0.0;
+  }
+}
+
+template <int NP, bool UNI, int NW, int E, int MS>
+__global__ __launch_bounds__(64 * NW) void k_step_rp(const double* __restrict__ uin,
                                                         double* __restrict__ rec,
                                                         double* __restrict__ last,
                                                         const double* __restrict__ scale,
@@ -120,17 +155,17 @@ __global__ __launch_bounds__(kBlock * W) void k_step_rp(const double* __restrict
 
 // Forward: MS LSERK4 steps of the tile; records u^{n0}..u^{n0+MS-1}'s jumps (and u^{n0+MS}'s
 // when the launch ends the sweep), writes u^{n0+MS} to `last`.  See step_tile (dg_advec.hip).
-template <int NP, bool UNI, int W, int E, int MS, bool EDGE>
+template <int NP, bool UNI, int NW, int E, int MS, bool EDGE>
 __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t tile,
                                              const double* __restrict__ uin,
                                              double* __restrict__ rec, double* __restrict__ last,
                                              const double* __restrict__ scale,
                                              const StepArgs<NP, 5, MS>& args) {
-  using G = RpGeo<NP, W, E>;
+  using G = RpGeo<NP, NW, E>;
   constexpr int NS = 5, T = G::T, LB = G::LB;
-  constexpr int H = MS * NS + 1;  // the stage cone + the final state's neighbours
+  constexpr int H = RpHalo<MS>::F;  // the stage cone + the final state's neighbours, even
   constexpr int TE = T - 2 * H;
-  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && E == 2, "pair tiles: aligned pairs");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
   constexpr int CB = G::kLds;  // lds[CB + st*NS + s] = inflow value of that stage
   constexpr int FB = LB + 2;   // one face array
@@ -138,17 +173,17 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
-  const int off = rp_load<NP, W, E, EDGE>(uin, e0, nd, lds);
+  const int off = rp_load<NP, NW, E, EDGE>(uin, e0, nd, lds);
   if constexpr (EDGE) {
     using SArgs = StepArgs<NP, NS, MS>;  // lane-indexed kernarg read, see step_tile
     const double* ka = reinterpret_cast<const double*>(
-        kernarg_tail<decltype(&k_step_rp<NP, UNI, W, E, MS>), SArgs>() + offsetof(SArgs, uin));
+        kernarg_tail<decltype(&k_step_rp<NP, UNI, NW, E, MS>), SArgs>() + offsetof(SArgs, uin));
     if (lane <= MS * NS) lds[CB + lane] = ka[lane];
   }
   __syncthreads();
   double ev[E][NE], od[E][NO];
   Elem El[E];
-  double sc[E];
+  double sc[E], jv[E];
 #pragma unroll
   for (int m = 0; m < E; ++m) {
     const int el = E * lane + m;
@@ -157,14 +192,10 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
     El[m] = elem_info<H, T, EDGE>(e0, el, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= El[m].inrange ? scale[El[m].kl] : 0.0;
-    // u^{n0}'s jumps (record n0-1) from the staged nodal values, as step_tile
-    if (args.n0 >= 1 && El[m].valid) {
-      const double uL = (EDGE && El[m].first) ? lds[CB] : us[-1];
-      const double uR = (EDGE && El[m].last) ? us[NP - 1] : us[NP];
-      const double du0 = us[0] - uL, du1 = us[NP - 1] - uR;
-      *rp_slot(rec, args.n0 - 1, args.ktot, El[m].e) = double2{du0 - du1, du0 + du1};
-    }
+    // u^{n0}'s left-face jumps (record n0-1) from the staged nodal values, as step_tile
+    jv[m] = us[0] - ((EDGE && El[m].first) ? lds[CB] : us[-1]);
   }
+  if (args.n0 >= 1) rp_rec_put<EDGE>(rec, args.n0 - 1, args.ktot, El, jv[0], jv[1]);
   __syncthreads();  // the image is read: the face arrays alias it
 
   double re[E][NE], ro[E][NO];
@@ -223,10 +254,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
           uR = El[m].last ? uN[m] : uR;
         }
         const double dlt = uR - uL, sig = -(uL + uR);
-        if (s == 0 && st >= 1 && El[m].valid) {  // u^{n0+st}'s jumps (record n0+st-1)
-          const double du0 = u0[m] - uL, du1 = uN[m] - uR;
-          *rp_slot(rec, args.n0 + st - 1, args.ktot, El[m].e) = double2{du0 - du1, du0 + du1};
-        }
+        if (s == 0) jv[m] = u0[m] - uL;  // u^{n0+st}'s left-face jump
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
           if constexpr (UNI) {
@@ -248,6 +276,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
           od[m][k] = fma(RK<NS>::B(s), ro[m][k], od[m][k]);
         }
       }
+      if (s == 0 && st >= 1) rp_rec_put<EDGE>(rec, args.n0 + st - 1, args.ktot, El, jv[0], jv[1]);
     }
   }
   if (args.jend) {
@@ -263,46 +292,40 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
     lds[fL + lane + 1] = u0[0];
     lds[fR + lane + 1] = uN[E - 1];
     __syncthreads();
-    const double fromL = lds[fR + lane], fromR = lds[fL + lane + 2];
+    const double fromL = lds[fR + lane];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
       double uL = (m == 0) ? fromL : uN[m - 1];
-      double uR = (m == E - 1) ? fromR : u0[m + 1];
-      if constexpr (EDGE) {
-        uL = El[m].first ? lds[CB + MS * NS] : uL;
-        uR = El[m].last ? uN[m] : uR;
-      }
-      if (El[m].valid) {
-        const double du0 = u0[m] - uL, du1 = uN[m] - uR;
-        *rp_slot(rec, args.n0 + MS - 1, args.ktot, El[m].e) = double2{du0 - du1, du0 + du1};
-      }
+      if constexpr (EDGE) uL = El[m].first ? lds[CB + MS * NS] : uL;
+      jv[m] = u0[m] - uL;
     }
+    rp_rec_put<EDGE>(rec, args.n0 + MS - 1, args.ktot, El, jv[0], jv[1]);
   }
   __syncthreads();  // the last face reads are done: the image is rewritten
-  rp_store<NP, W, E, H, EDGE>(last, tile * TE * NP, nd, lds, ev, od, false);
+  rp_store<NP, NW, E, H, EDGE>(last, tile * TE * NP, nd, lds, ev, od, false);
 }
 
-template <int NP, bool UNI, int W, int E, int MS>
-__global__ __launch_bounds__(kBlock * W) void k_step_rp(const double* __restrict__ uin,
+template <int NP, bool UNI, int NW, int E, int MS>
+__global__ __launch_bounds__(64 * NW) void k_step_rp(const double* __restrict__ uin,
                                                         double* __restrict__ rec,
                                                         double* __restrict__ last,
                                                         const double* __restrict__ scale,
                                                         StepArgs<NP, 5, MS> args) {
-  using G = RpGeo<NP, W, E>;
+  using G = RpGeo<NP, NW, E>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
-  constexpr int H = MS * 5 + 1;
+  constexpr int H = RpHalo<MS>::F;
   const int64_t e0 = tile * (G::T - 2 * H) - H;
   if (edge_tile(e0, G::T, args.ktot, args.K))
-    rp_step_tile<NP, UNI, W, E, MS, true>(lds, tile, uin, rec, last, scale, args);
+    rp_step_tile<NP, UNI, NW, E, MS, true>(lds, tile, uin, rec, last, scale, args);
   else
-    rp_step_tile<NP, UNI, W, E, MS, false>(lds, tile, uin, rec, last, scale, args);
+    rp_step_tile<NP, UNI, NW, E, MS, false>(lds, tile, uin, rec, last, scale, args);
 }
 
 // Adjoint: MS reverse steps st = MS-1..0 of the tile, each
 //   eta += DWR(u^{n0+st+1}'s recorded jumps, w^{n0+st+1});  w^{n0+st} = S^T w^{n0+st+1}
 // (terminal functionals only: no source).  See adj_tile (dg_advec.hip).
-template <int NP, bool UNI, int W, int E, int MS, bool EDGE>
+template <int NP, bool UNI, int NW, int E, int MS, bool EDGE>
 __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t tile,
                                             const double* __restrict__ win,
                                             double* __restrict__ wout,
@@ -310,29 +333,24 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
                                             double* __restrict__ eta,
                                             const double* __restrict__ scale,
                                             const AdjArgs<NP, MS>& args) {
-  using G = RpGeo<NP, W, E>;
+  using G = RpGeo<NP, NW, E>;
   constexpr int NS = 5, T = G::T, LB = G::LB;
-  constexpr int H = MS * NS;
+  constexpr int H = RpHalo<MS>::A;
   constexpr int TE = T - 2 * H;
-  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && E == 2, "pair tiles: aligned pairs");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   constexpr int FB = LB + 2;
   const int lane = threadIdx.x;
   const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
+  const int64_t ea = e0 + E * lane;  // the lane's first element (even)
 
-  const int off = rp_load<NP, W, E, EDGE>(win, e0, nd, lds);
-  // the jumps of u^{n0+st+1} (record n0+st): one 16-byte load per element and step,
-  // prefetched a step ahead
-  double2 jn[E];
-  bool jin[E];
-#pragma unroll
-  for (int m = 0; m < E; ++m) {
-    const int64_t e = e0 + E * lane + m;
-    jin[m] = e >= 0 && e < args.ktot;
-    jn[m] = jin[m] ? *rp_slot(const_cast<double*>(rec), args.n0 + MS - 1, args.ktot, e)
-                   : double2{0.0, 0.0};
-  }
+  const int off = rp_load<NP, NW, E, EDGE>(win, e0, nd, lds);
+  // the left-face jumps of u^{n0+st+1} (record n0+st) of the lane's two elements and of its
+  // right neighbour: one 16-byte and one 8-byte load per lane and step, prefetched a step ahead
+  double2 jn;
+  double jn2;
+  rp_rec_get<EDGE>(rec, args.n0 + MS - 1, args.ktot, ea, jn, jn2);
   __syncthreads();
   double we[E][NE], wo[E][NO];
   Elem El[E];
@@ -356,14 +374,10 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
 
 #pragma unroll 1
   for (int st = MS - 1; st >= 0; --st) {
-    double2 jc[E];
-#pragma unroll
-    for (int m = 0; m < E; ++m) {
-      jc[m] = jn[m];
-      if (st > 0 && jin[m])
-        jn[m] = *rp_slot(const_cast<double*>(rec), args.n0 + st - 1, args.ktot,
-                         e0 + E * lane + m);
-    }
+    // du0 = j_e; du1 = -j_{e+1} (0 at a trajectory's last element): du0 - du1 and du0 + du1
+    // are the snapshot path's doubles bit for bit (dg_common.h rec_ld)
+    const double jc[E + 1] = {jn.x, jn.y, jn2};
+    if (st > 0) rp_rec_get<EDGE>(rec, args.n0 + st - 1, args.ktot, ea, jn, jn2);
     if (args.has_eta) {
 #pragma unroll
       for (int m = 0; m < E; ++m) {
@@ -372,7 +386,10 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
         for (int k = 0; k < NE; ++k) pe = fma(args.op.le[k], we[m][k], pe);
 #pragma unroll
         for (int k = 0; k < NO; ++k) po = fma(args.op.lo[k], wo[m][k], po);
-        double c = fma(jc[m].x, pe, jc[m].y * po);
+        const bool lst = EDGE && El[m].last;
+        const double dd = lst ? jc[m] : jc[m] + jc[m + 1];
+        const double ds = lst ? jc[m] : jc[m] - jc[m + 1];
+        double c = fma(dd, pe, ds * po);
         if constexpr (!UNI) c *= sc[m];
         eacc[m] += c;
       }
@@ -461,28 +478,28 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
   for (int m = 0; m < E; ++m)
     if (args.has_eta && El[m].valid) eta_update(eta, El[m].e, eacc[m], args.has_eta);
   __syncthreads();  // the last face reads are done: the image is rewritten
-  rp_store<NP, W, E, H, EDGE>(wout, tile * TE * NP, nd, lds, we, wo, true);
+  rp_store<NP, NW, E, H, EDGE>(wout, tile * TE * NP, nd, lds, we, wo, true);
 }
 
-template <int NP, bool UNI, int W, int E, int MS>
-__global__ __launch_bounds__(kBlock * W) void k_adj_rp(const double* __restrict__ win,
+template <int NP, bool UNI, int NW, int E, int MS>
+__global__ __launch_bounds__(64 * NW) void k_adj_rp(const double* __restrict__ win,
                                                        double* __restrict__ wout,
                                                        const double* __restrict__ rec,
                                                        double* __restrict__ eta,
                                                        const double* __restrict__ scale,
                                                        AdjArgs<NP, MS> args) {
-  using G = RpGeo<NP, W, E>;
+  using G = RpGeo<NP, NW, E>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
-  constexpr int H = MS * 5;
+  constexpr int H = RpHalo<MS>::A;
   const int64_t e0 = tile * (G::T - 2 * H) - H;
   if (edge_tile(e0, G::T, args.ktot, args.K))
-    rp_adj_tile<NP, UNI, W, E, MS, true>(lds, tile, win, wout, rec, eta, scale, args);
+    rp_adj_tile<NP, UNI, NW, E, MS, true>(lds, tile, win, wout, rec, eta, scale, args);
   else
-    rp_adj_tile<NP, UNI, W, E, MS, false>(lds, tile, win, wout, rec, eta, scale, args);
+    rp_adj_tile<NP, UNI, NW, E, MS, false>(lds, tile, win, wout, rec, eta, scale, args);
 }
 
-template <int NP, int W, int E, int MS>
+template <int NP, int NW, int E, int MS>
 int rp_step_e(const dg_plan* p, const double* in, double* rec, double* last, const double* times,
               double dt, hipStream_t st, int64_t n0, bool jend) {
   StepArgs<NP, 5, MS> a;
@@ -497,19 +514,19 @@ int rp_step_e(const dg_plan* p, const double* in, double* rec, double* last, con
   a.K = int32_t(p->K);
   a.xcd = p->xcd_order;
   a.jend = jend ? 1 : 0;
-  constexpr int TE = RpGeo<NP, W, E>::T - 2 * (MS * 5 + 1);
+  constexpr int TE = RpGeo<NP, NW, E>::T - 2 * RpHalo<MS>::F;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_step_rp<NP, true, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
+    hipLaunchKernelGGL((k_step_rp<NP, true, NW, E, MS>), dim3(grid), dim3(64 * NW), 0, st, in,
                        rec, last, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_step_rp<NP, false, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, in,
+    hipLaunchKernelGGL((k_step_rp<NP, false, NW, E, MS>), dim3(grid), dim3(64 * NW), 0, st, in,
                        rec, last, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-template <int NP, int W, int E, int MS>
+template <int NP, int NW, int E, int MS>
 int rp_adj_e(const dg_plan* p, const double* win, double* wout, const double* rec, double* eta,
              int eta_mode, const double* t_next, double dt, hipStream_t st, int64_t n0) {
   AdjArgs<NP, MS> a;
@@ -525,50 +542,54 @@ int rp_adj_e(const dg_plan* p, const double* win, double* wout, const double* re
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr ? (eta_mode | kEtaOn) : 0;
   a.xcd = p->xcd_order;
-  constexpr int TE = RpGeo<NP, W, E>::T - 2 * MS * 5;
+  constexpr int TE = RpGeo<NP, NW, E>::T - 2 * RpHalo<MS>::A;
   const unsigned grid = grid_for(p->ktot, TE);
   if (p->uniform)
-    hipLaunchKernelGGL((k_adj_rp<NP, true, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+    hipLaunchKernelGGL((k_adj_rp<NP, true, NW, E, MS>), dim3(grid), dim3(64 * NW), 0, st, win,
                        wout, rec, eta, p->d_scale, a);
   else
-    hipLaunchKernelGGL((k_adj_rp<NP, false, W, E, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+    hipLaunchKernelGGL((k_adj_rp<NP, false, NW, E, MS>), dim3(grid), dim3(64 * NW), 0, st, win,
                        wout, rec, eta, p->d_scale, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-// Shapes: 2 elements per lane, tile width 1 or 2 (512 or 1024 elements per tile), 1, 2, 4, 5,
-// 8, 10, 16 or 20 steps per launch (16 and 20 only at width 2: the cone leaves too few output
-// elements of a 512-element tile); Np <= 8.
-template <int NP, int W>
+// Shapes: 2 elements per lane on workgroups of NW = 4 or 8 waves (the plan's rec_tile_width
+// 1 / 2: tiles of 512 / 1024 elements), 1, 2, 4, 5, 8, 10, 16 or 20 steps per launch (16 and 20
+// only at NW = 8: the cone leaves too few output elements of a 512-element tile); Np <= 9.
+// Wider workgroups (10, 12, 16 waves: less halo per tile, and 10 waves fill the adjoint's 5
+// waves per SIMD) were measured slower in both directions (profiles/r03/waves/: adjoint
+// 180 -> 200-244 us per sweep, forward 157-166 -> 183-220 us): the per-stage barrier waits
+// for more waves.
+template <int NP, int NW>
 int rp_step_w(const dg_plan* p, int ms, const double* in, double* rec, double* last,
               const double* times, double dt, hipStream_t st, int64_t n0, bool jend) {
   switch (ms) {
-    case 20: if constexpr (W == 2) return rp_step_e<NP, W, 2, 20>(p, in, rec, last, times, dt, st, n0, jend); break;
-    case 16: if constexpr (W == 2) return rp_step_e<NP, W, 2, 16>(p, in, rec, last, times, dt, st, n0, jend); break;
-    case 10: return rp_step_e<NP, W, 2, 10>(p, in, rec, last, times, dt, st, n0, jend);
-    case 8: return rp_step_e<NP, W, 2, 8>(p, in, rec, last, times, dt, st, n0, jend);
-    case 5: return rp_step_e<NP, W, 2, 5>(p, in, rec, last, times, dt, st, n0, jend);
-    case 4: return rp_step_e<NP, W, 2, 4>(p, in, rec, last, times, dt, st, n0, jend);
-    case 2: return rp_step_e<NP, W, 2, 2>(p, in, rec, last, times, dt, st, n0, jend);
-    case 1: return rp_step_e<NP, W, 2, 1>(p, in, rec, last, times, dt, st, n0, jend);
+    case 20: if constexpr (NW == 8) return rp_step_e<NP, NW, 2, 20>(p, in, rec, last, times, dt, st, n0, jend); break;
+    case 16: if constexpr (NW == 8) return rp_step_e<NP, NW, 2, 16>(p, in, rec, last, times, dt, st, n0, jend); break;
+    case 10: return rp_step_e<NP, NW, 2, 10>(p, in, rec, last, times, dt, st, n0, jend);
+    case 8: return rp_step_e<NP, NW, 2, 8>(p, in, rec, last, times, dt, st, n0, jend);
+    case 5: return rp_step_e<NP, NW, 2, 5>(p, in, rec, last, times, dt, st, n0, jend);
+    case 4: return rp_step_e<NP, NW, 2, 4>(p, in, rec, last, times, dt, st, n0, jend);
+    case 2: return rp_step_e<NP, NW, 2, 2>(p, in, rec, last, times, dt, st, n0, jend);
+    case 1: return rp_step_e<NP, NW, 2, 1>(p, in, rec, last, times, dt, st, n0, jend);
     default: break;
   }
   return fail(DG_ERR_ARG, "pair tiles: unsupported steps per launch for this tile width");
 }
 
-template <int NP, int W>
+template <int NP, int NW>
 int rp_adj_w(const dg_plan* p, int ms, const double* win, double* wout, const double* rec,
              double* eta, int em, const double* t_next, double dt, hipStream_t st, int64_t n0) {
   switch (ms) {
-    case 20: if constexpr (W == 2) return rp_adj_e<NP, W, 2, 20>(p, win, wout, rec, eta, em, t_next, dt, st, n0); break;
-    case 16: if constexpr (W == 2) return rp_adj_e<NP, W, 2, 16>(p, win, wout, rec, eta, em, t_next, dt, st, n0); break;
-    case 10: return rp_adj_e<NP, W, 2, 10>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
-    case 8: return rp_adj_e<NP, W, 2, 8>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
-    case 5: return rp_adj_e<NP, W, 2, 5>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
-    case 4: return rp_adj_e<NP, W, 2, 4>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
-    case 2: return rp_adj_e<NP, W, 2, 2>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
-    case 1: return rp_adj_e<NP, W, 2, 1>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 20: if constexpr (NW == 8) return rp_adj_e<NP, NW, 2, 20>(p, win, wout, rec, eta, em, t_next, dt, st, n0); break;
+    case 16: if constexpr (NW == 8) return rp_adj_e<NP, NW, 2, 16>(p, win, wout, rec, eta, em, t_next, dt, st, n0); break;
+    case 10: return rp_adj_e<NP, NW, 2, 10>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 8: return rp_adj_e<NP, NW, 2, 8>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 5: return rp_adj_e<NP, NW, 2, 5>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 4: return rp_adj_e<NP, NW, 2, 4>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 2: return rp_adj_e<NP, NW, 2, 2>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
+    case 1: return rp_adj_e<NP, NW, 2, 1>(p, win, wout, rec, eta, em, t_next, dt, st, n0);
     default: break;
   }
   return fail(DG_ERR_ARG, "pair tiles: unsupported steps per launch for this tile width");
@@ -577,16 +598,16 @@ int rp_adj_w(const dg_plan* p, int ms, const double* win, double* wout, const do
 template <int NP>
 int rp_step_np(const dg_plan* p, int ms, const double* in, double* rec, double* last,
                const double* times, double dt, hipStream_t st, int64_t n0, bool jend) {
-  if (p->rec_tile_width == 2) return rp_step_w<NP, 2>(p, ms, in, rec, last, times, dt, st, n0, jend);
-  return rp_step_w<NP, 1>(p, ms, in, rec, last, times, dt, st, n0, jend);
+  if (rec_fwd_width(p) == 2) return rp_step_w<NP, 8>(p, ms, in, rec, last, times, dt, st, n0, jend);
+  return rp_step_w<NP, 4>(p, ms, in, rec, last, times, dt, st, n0, jend);
 }
 
 template <int NP>
 int rp_adj_np(const dg_plan* p, int ms, const double* win, double* wout, const double* rec,
               double* eta, int em, const double* t_next, double dt, hipStream_t st, int64_t n0) {
   if (p->rec_tile_width == 2)
-    return rp_adj_w<NP, 2>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
-  return rp_adj_w<NP, 1>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    return rp_adj_w<NP, 8>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+  return rp_adj_w<NP, 4>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
 }
 
 }  // namespace
@@ -603,7 +624,8 @@ int pair_launch_step_rec(const dg_plan* p, int ms, const double* in, double* rec
     case 6: return rp_step_np<6>(p, ms, in, rec, last, times, dt, st, n0, jend);
     case 7: return rp_step_np<7>(p, ms, in, rec, last, times, dt, st, n0, jend);
     case 8: return rp_step_np<8>(p, ms, in, rec, last, times, dt, st, n0, jend);
-    default: return fail(DG_ERR_ARG, "pair tiles support Np <= 8");
+    case 9: return rp_step_np<9>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    default: return fail(DG_ERR_ARG, "pair tiles support Np <= 9");
   }
 }
 
@@ -618,7 +640,8 @@ int pair_launch_adj_rec(const dg_plan* p, int ms, const double* win, double* wou
     case 6: return rp_adj_np<6>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
     case 7: return rp_adj_np<7>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
     case 8: return rp_adj_np<8>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
-    default: return fail(DG_ERR_ARG, "pair tiles support Np <= 8");
+    case 9: return rp_adj_np<9>(p, ms, win, wout, rec, eta, em, t_next, dt, st, n0);
+    default: return fail(DG_ERR_ARG, "pair tiles support Np <= 9");
   }
 }
 

@@ -73,8 +73,8 @@ class EnsembleSweep:
     amp, freq, phase = params if params is not None else ic_params(self.ic_indices, seed_base)
     if record == "jumps":
       # The snapshot-free pair (dg_lserk4_fwd_rec / dg_lserk4_adj_rec): the forward keeps
-      # per element and step only the two face jumps the indicator needs (16 B instead of
-      # 8 Np B).  At equal steps per launch w, eta and the refine decision are bit-identical
+      # per element and step only the left-face jump the indicator needs (8 B instead of
+      # 8 Np B; the right face's is the next element's).  At equal steps per launch w, eta and the refine decision are bit-identical
       # to the snapshot pair's; at the record pair's own (longer) launches the states differ
       # in the last bits and eta by the indicator's conditioning (~1e-9 relative on smooth
       # solutions, DESIGN.md §5 "The indicator's conditioning").

@@ -112,6 +112,9 @@ class DGAdvection1D:
     self.rec_steps_per_launch = int(r[1])
     self.rec_lane_elements = int(r[2])
     self.rec_fwd_steps_per_launch = int(r[3])
+    f = (ctypes.c_int64 * 2)()
+    _lib.check(self._lib.dg_plan_query_rec_fwd(self._plan, f), "dg_plan_query_rec_fwd")
+    self.rec_fwd_tile_width = int(f[0])
 
   # --- lifetime ---
   def close(self):
@@ -133,7 +136,7 @@ class DGAdvection1D:
 
   def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None,
            rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
-           rec_fwd_steps_per_launch=None):
+           rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -144,11 +147,14 @@ class DGAdvection1D:
     ``rec_lane_elements`` = 2 runs them with two consecutive elements per lane (tiles of
     512*``rec_tile_width`` elements, bit-identical at equal steps per launch);
     ``rec_fwd_steps_per_launch`` gives the forward its own steps per launch (setting
-    ``rec_steps_per_launch`` applies to both directions and clears it)."""
+    ``rec_steps_per_launch`` applies to both directions and clears it);
+    ``rec_fwd_tile_width`` likewise gives the forward its own tile width (0: the adjoint's;
+    setting ``rec_tile_width`` applies to both)."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
                      (_lib.DG_TUNE_REC_LANE_ELEMENTS, rec_lane_elements),
-                     (_lib.DG_TUNE_REC_FWD_STEPS_PER_LAUNCH, rec_fwd_steps_per_launch)):
+                     (_lib.DG_TUNE_REC_FWD_STEPS_PER_LAUNCH, rec_fwd_steps_per_launch),
+                     (_lib.DG_TUNE_REC_FWD_TILE_WIDTH, rec_fwd_tile_width)):
       if val is not None:
         _lib.check(self._lib.dg_plan_tune(self._plan, key, int(val)), "dg_plan_tune")
     if xcd_order is not None:
@@ -269,17 +275,23 @@ class DGAdvection1D:
     return w, eta
 
   # --- snapshot-free sweep pair (linear LSERK4 plans, terminal functionals) ---
+  @property
+  def jump_ld(self):
+    """Row length of the jump record: batch*K rounded up to even (16-byte aligned rows)."""
+    return (self.ktot + 1) & ~1
+
   def new_jumps(self, nsteps):
-    """A jump record for an ``nsteps`` sweep: (nsteps, batch*K, 2) float64."""
-    return torch.empty((int(nsteps), self.ktot, 2), dtype=torch.float64, device=self.device)
+    """A jump record for an ``nsteps`` sweep: (nsteps, jump_ld) float64; row n-1, entry e is
+    u^n's left-face jump u_0 - uL of element e (include/dg_advec.h)."""
+    return torch.empty((int(nsteps), self.jump_ld), dtype=torch.float64, device=self.device)
 
   def _jumps(self, jumps, nsteps):
-    return self._field(jumps, "jumps", 2 * int(nsteps) * self.ktot)
+    return self._field(jumps, "jumps", int(nsteps) * self.jump_ld)
 
   def forward_rec(self, u0, t0, dt, nsteps, jumps, out=None):
     """``nsteps`` LSERK4 steps from u0 into ``out`` (default: in place on u0), recording
-    per element and step the two interelement jumps of each state u^1..u^nsteps instead of
-    the states (dg_lserk4_fwd_rec: 16 bytes per element-step for 8*Np).  With
+    per element and step the left-face jump of each state u^1..u^nsteps instead of the states
+    (dg_lserk4_fwd_rec: 8 bytes per element-step for 8*Np).  With
     ``adjoint_rec`` this is the snapshot sweep pair with src_coef = 0, bit for bit."""
     out = u0 if out is None else out
     rc = self._lib.dg_lserk4_fwd_rec(self._plan, self._field(u0, "u0"), self._field(out, "out"),

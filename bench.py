@@ -516,7 +516,7 @@ def indicator_resolution(sweep, N, K):
   import torch
   with torch.no_grad():
     if sweep.record == "jumps":
-      jmax = float(sweep.jumps.abs().max())  # (du0 - du1, du0 + du1): |du| <= max of the two
+      jmax = float(sweep.jumps[:, :sweep.op.ktot].abs().max())  # the left-face jumps
       umax = float(sweep.u0.abs().max())
     else:
       # the jump indicator's adjoint runs in place on snapshot N; u^{N-1} is intact
@@ -634,16 +634,16 @@ def main(argv=None):
   #   snapshots: forward reads u^n once and writes the m snapshots u^{n+1..n+m}: (8 + 8 m) B
   #     per DOF; the adjoint reads w^{n+m} and the m snapshots and writes w^n: (16 + 8 m) B
   #     per DOF, plus the indicator read-modify-write, 16 B per element;
-  #   jumps: forward reads u^n, writes u^{n+m} and m jump pairs: 16 B per DOF + 16 m B per
-  #     element; the adjoint reads w^{n+m} and m jump pairs, writes w^n, updates eta:
-  #     16 B per DOF + (16 m + 16) B per element.
+  #   jumps: forward reads u^n, writes u^{n+m} and m left-face jumps: 16 B per DOF + 8 m B per
+  #     element; the adjoint reads w^{n+m} and m jump rows, writes w^n, updates eta:
+  #     16 B per DOF + (8 m + 16) B per element.
   # A sweep's launches may differ in m (e.g. 8 + 8 + 4 at 20 steps); the per-launch figures
   # are the sweep's averages: achieved = sweep bytes / sweep time.
   #   p-estimate (k_adj_p): reads w^{n+m} and writes w^n at order N+1 (16 (Np + 1) B per
   #     element), reads the m + 1 order-N snapshots u^n..u^{n+m} (8 (m + 1) Np B), updates eta.
   if args.record == "jumps":
-    fwd_bytes = float(np.mean([(16.0 * Np + 16.0 * m) * ktot for m in fchunks]))
-    adj_bytes = float(np.mean([(16.0 * Np + 16.0 * m + 16.0) * ktot for m in chunks]))
+    fwd_bytes = float(np.mean([(16.0 * Np + 8.0 * m) * ktot for m in fchunks]))
+    adj_bytes = float(np.mean([(16.0 * Np + 8.0 * m + 16.0) * ktot for m in chunks]))
   elif pmode:
     fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 * (Np + 1) + 8.0 * (m + 1) * Np + 16.0) * ktot
@@ -656,20 +656,29 @@ def main(argv=None):
   kadj, kstep = ("k_adj_rp", "k_step_rp") if pairs else ("k_adj", "k_step")
   if pmode:
     kadj = "k_adj_p"
-  tile_tag = f"{tw},2 elements/lane" if pairs else f"{tw}"
+  tile_tag = tile_tag_fwd = f"{tw},2 elements/lane" if pairs else f"{tw}"
   # Issued vs useful lanes: each tile recomputes a halo of H elements per side (the
   # dependency cone of its fused steps) and writes T - 2H, weighted by steps.
-  if args.record == "jumps":
-    T_adj = T_fwd = 256 * tw * (2 if pairs else 1)
+  if pairs:
+    # pair tiles: 512 elements per tile width; halos rounded up to even (aligned record
+    # pairs, dg_rec.hip RpHalo), the forward's one wider for the final jumps
+    T_of = lambda m, fwd: 512 * tw  # noqa: E731
+    h_fwd = lambda m: (5 * m + 2) & ~1  # noqa: E731
+    h_adj = lambda m: (5 * m + 1) & ~1  # noqa: E731
+  elif args.record == "jumps":
+    T_of = lambda m, fwd: 256 * tw  # noqa: E731
     h_fwd = lambda m: 5 * m + 1  # noqa: E731  (the final state's jumps need one more)
+    h_adj = lambda m: 5 * m  # noqa: E731
   else:
-    T_adj = 256 * tw
     # the snapshot forward runs on 256-element one-wave tiles (4 elements per lane) at N <= 2
     # by default (dg_plan_create), else on workgroup tiles of 256 * tile width
     T_fwd = 256 if N <= 2 else 256 * sweep.op.tile_width
-    h_fwd = lambda m: 5 * m  # noqa: E731
-  halo_adj = float(np.average([halo_factor(T_adj, 5 * m) for m in chunks], weights=chunks))
-  halo_fwd = float(np.average([halo_factor(T_fwd, h_fwd(m)) for m in fchunks], weights=fchunks))
+    T_of = lambda m, fwd: T_fwd if fwd else 256 * tw  # noqa: E731
+    h_fwd = h_adj = lambda m: 5 * m  # noqa: E731
+  halo_adj = float(np.average([halo_factor(T_of(m, False), h_adj(m)) for m in chunks],
+                              weights=chunks))
+  halo_fwd = float(np.average([halo_factor(T_of(m, True), h_fwd(m)) for m in fchunks],
+                              weights=fchunks))
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
@@ -746,13 +755,13 @@ def main(argv=None):
                    "note": ("p-estimate: per reverse step the order-(N+1) forward step from the "
                             "prolonged snapshot and the order-(N+1) reverse step (roofline_fp64)"
                             if pmode else None if args.record != "jumps" else
-                            "jump record: 16 B per element-step instead of an 8 Np B snapshot, so "
+                            "jump record: 8 B per element-step instead of an 8 Np B snapshot, so "
                             "the launches are bound by fp64 issue and the per-stage barrier "
                             "chain, not HBM (roofline_fp64); the snapshot sweep's k_adj reaches "
                             "0.62 of HBM (--record snapshots, DESIGN.md section 7)")},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_gbs / HBM_PEAK_GBS,
-                       "kernel": f"{kstep}<{Np},uniform,{tile_tag},{fms}{rec_tag}> ({fms} steps per launch)",
+                       "kernel": f"{kstep}<{Np},uniform,{tile_tag_fwd},{fms}{rec_tag}> ({fms} steps per launch)",
                        "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
       "roofline_effective": effective,

@@ -91,39 +91,44 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             on one-wave tiles of 64*value elements, value consecutive
  *                             elements per lane, cross-lane faces by DPP (LSERK4, Np <= 8;
  *                             bit-identical to the workgroup tiles at equal steps per launch)
- *   DG_TUNE_REC_TILE_WIDTH    1 or 2: tile width of the jump-record sweeps
+ *   DG_TUNE_REC_TILE_WIDTH    1 or 2: tile width of the jump-record sweeps, both directions
  *                             (dg_lserk4_fwd_rec / dg_lserk4_adj_rec): workgroups of 256*value
- *                             lanes (default 2)
+ *                             lanes (default 2; at Np = 9 1 for the adjoint, 2 for the forward)
+ *   DG_TUNE_REC_FWD_TILE_WIDTH  the forward record sweep's own tile width (0: as the adjoint's)
  *   DG_TUNE_REC_STEPS_PER_LAUNCH  their steps per launch, both directions (default 10): 1, 2,
  *                             4, 5, 8, 10, 16
  *                             or 20 on pair tiles (16 and 20 need tile width 2, else 8 / 10
  *                             are used), a sweep chunked by halving (20 -> 10 -> 5 -> 2 -> 1);
  *                             1, 2, 4 or 8 on one element per lane (8 needs tile width 2,
- *                             else 4); Np = 9 caps it at 2
+ *                             else 4; Np = 9 caps those at 2)
  *   DG_TUNE_REC_FWD_STEPS_PER_LAUNCH  the forward record sweep's own steps per launch (same
  *                             values; default by size: 20 on 1024-element pair tiles up to
  *                             3*2^20 elements per plan, else as the adjoint; setting
  *                             DG_TUNE_REC_STEPS_PER_LAUNCH makes it "as the adjoint")
  *   DG_TUNE_REC_LANE_ELEMENTS 1 or 2: consecutive elements per lane of the jump-record sweeps'
  *                             workgroup tiles (default 2: tiles of 512*width elements,
- *                             lane-internal faces in registers; Np <= 8; bit-identical to 1 at
+ *                             lane-internal faces in registers; bit-identical to 1 at
  *                             equal steps per launch)
  *   DG_TUNE_P_TILE_WIDTH      1 or 2: tile width of the p-enriched estimate (dg_lserk4_adj_p):
  *                             workgroups of 256*value lanes, one element per lane (default 2)
  *   DG_TUNE_P_STEPS_PER_LAUNCH its steps per launch: 1, 2, 4 (default) or 8 (8 needs tile
  *                             width 2, else 4); a sweep is chunked by halving
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
- * DG_REC_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
+ * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
  * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
-       DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10 };
+       DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10,
+       DG_TUNE_REC_FWD_TILE_WIDTH = 11 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
  * (adjoint), out[2] = elements per lane, out[3] = the forward's steps per launch. */
 int dg_plan_query_rec(const dg_plan* plan, int64_t out[4]);
+
+/* The forward record sweep's shape: out[0] = tile width, out[1] = steps per launch. */
+int dg_plan_query_rec_fwd(const dg_plan* plan, int64_t out[2]);
 
 /* The p-enriched estimate's effective shape: out[0] = tile width, out[1] = steps per launch. */
 int dg_plan_query_p(const dg_plan* plan, int64_t out[2]);
@@ -217,14 +222,18 @@ int dg_lserk4_adj_ex(dg_plan* plan, double* w, const double* snapshots, double t
 /* Snapshot-free sweep pair (linear flux, LSERK4).  For the linear advection operator the
  * adjoint S^T does not depend on the state, and the indicator needs of each u^n only the two
  * interelement jumps per element (R = LIFT*(Fscale.*du), utils/AdvecRHS1D.m:19: du0 at the
- * left face, du1 at the right face, inflow / outflow rules as in AdvecRHS1D).  The forward
- * records them instead of the states: 16 bytes per element and step where a snapshot takes
+ * left face, du1 at the right face, inflow / outflow rules as in AdvecRHS1D).  A face's jump
+ * is shared by its two elements (element e's du1 = -du0 of element e+1, exactly; 0 at a
+ * trajectory's last element), so the forward records one number per element and step, the
+ * left-face jump, instead of the states: 8 bytes per element and step where a snapshot takes
  * 8*Np.  w, eta and the final state are bit-identical to the dg_lserk4_fwd + dg_lserk4_adj_ex
  * sweep pair with src_coef = 0 (terminal functionals, e.g. J = |u^N|^2/2 with w = u^N).
  *
  * dg_lserk4_fwd_rec: uN = u^nsteps from u0 = u^0 (u0 untouched unless uN == u0).
- *   jumps (device, 16-byte aligned, 2*nsteps*batch*K doubles): for n = 1..nsteps and element
- *   e, jumps[2*((n-1)*batch*K + e) + {0, 1}] = {du0 - du1, du0 + du1} of u^n at t_n.
+ *   jumps (device, 16-byte aligned, nsteps*LD doubles with LD = batch*K rounded up to even):
+ *   for n = 1..nsteps and element e, jumps[(n-1)*LD + e] = du0 = u_0 - uL of u^n at t_n (uL:
+ *   element e-1's u_N, or the inflow value at a trajectory's first element); the pad entry of
+ *   an odd batch*K is not written.
  * dg_lserk4_adj_rec: dg_lserk4_adj_ex(w, snapshots, src_coef = 0, eta, flags) with the
  *   record of the same sweep in place of the snapshots (required whenever nsteps > 0, also
  *   without eta: DG_ERR_ARG otherwise). */

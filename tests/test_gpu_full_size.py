@@ -105,13 +105,13 @@ def test_full_size_config2_record_default(pkg, gpu, N):
   (measured: 0.9 % of max|eta| between the GPU and the oracle); with O(0.1) jumps the
   indicator is as well conditioned as the states.  The refine index must equal the oracle's
   when the oracle's top two |eta| are apart by more than the bar.  N = 1 and 8 (config 5's
-  ends; Np = 9 runs the one-element-per-lane record kernels, 2 steps per launch) as well."""
+  ends; pair tiles at every Np since round 3) as well."""
   import torch
   K, nsteps = 1 << 20, 20
   _, v_x, _, _ = setup1d.mesh_gen1d(0.0, 1.0, K)
   S = setup1d.startup1d(N, v_x, metric="element")
   op = pkg.operators.DGAdvection1D(pkg.BaseGalerkin1D(n=N, v_x=v_x))
-  assert (op.rec_lane_elements, op.rec_steps_per_launch) == ((2, 10) if N < 8 else (1, 2))
+  assert (op.rec_lane_elements, op.rec_steps_per_launch) == (2, 10)
   u0 = np.sin(2 * np.pi * S["x"]) + 0.1 * np.random.default_rng(2).standard_normal(S["x"].shape)
   dt = oadv.bench_dt(S)
   ref, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, A, S)

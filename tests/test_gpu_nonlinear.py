@@ -343,8 +343,16 @@ def test_diverged_sweep_is_refused(pkg, gpu):
 
 def window_setup(N, v_x, k0, k1, s_glob):
   """The oracle's setup on elements [k0, k1) of a uniform mesh, with the plan's global
-  metric 2/mean(h) (the window's own mean differs in the last bit)."""
-  S = setup1d.startup1d(N, v_x[k0:k1 + 1], metric="element")
+  metric 2/mean(h) (the window's own mean differs in the last bit).
+
+  The window's coordinates start at 0 (v_x[k0] subtracted; exact on mesh_gen1d's dyadic
+  vertices).  SlopeLimitLin.m:10-11 forms h = x_N - x_0 and x - x0 from nodal coordinates,
+  which at x ~ 0.5 and h = 2^-22 carry relative rounding of eps*|x|/h ~ 2e-10; the kernels use
+  h*r/2 (exact).  Only differences of x enter the limiter, so the shift changes nothing but
+  that rounding: measured on this test's jump window, the unshifted oracle's one-step forward
+  differs from the GPU's by 1.7e-11 and its adjoint by 2.7e-10 of max|w|, the shifted one by
+  1.8e-15 and 1.4e-14."""
+  S = setup1d.startup1d(N, v_x[k0:k1 + 1] - v_x[k0], metric="element")
   S["rx"][:] = s_glob
   S["Fscale"][:] = s_glob
   S["J"][:] = 1.0 / s_glob

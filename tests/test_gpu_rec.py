@@ -2,8 +2,10 @@
 
 For linear advection the adjoint step S^T does not depend on the state and the indicator
 needs of each u^n only its two interelement jumps per element (R = LIFT*(Fscale.*du),
-utils/AdvecRHS1D.m:19).  The forward records (du0 - du1, du0 + du1) per element and step in
-place of the snapshots.  Bars:
+utils/AdvecRHS1D.m:19); a face's jump is shared by its two elements, so the forward records
+one number per element and step in place of the snapshots: the left-face jump du0 = u_0 - uL
+(element e's right-face du1 is -du0 of element e+1, or 0 at a trajectory's last element).
+Bars:
   * the record equals the jumps of the snapshot sweep's states, bit for bit (same doubles,
     same subtractions), and agrees with the oracle's AdvecRHS1D face jumps (face_jumps,
     which carry the (a nx)/2 factors) to rounding;
@@ -25,14 +27,11 @@ def host(t):
 
 
 def raw_jumps(u_em, K, batch, Np, uin):
-  """(du0 - du1, du0 + du1) per element of an element-major field: du0 = u_0 - (left
-  neighbour's u_N, or the inflow value), du1 = u_N - (right neighbour's u_0, or u_N)."""
+  """The left-face jump du0 = u_0 - (left neighbour's u_N, or the inflow value) per element
+  of an element-major field, (batch*K,)."""
   u = u_em.reshape(batch, K, Np)
   left = np.concatenate([np.full((batch, 1), uin), u[:, :-1, Np - 1]], axis=1)
-  right = np.concatenate([u[:, 1:, 0], u[:, -1:, Np - 1]], axis=1)
-  du0 = u[:, :, 0] - left
-  du1 = u[:, :, Np - 1] - right
-  return np.stack([du0 - du1, du0 + du1], axis=-1).reshape(batch * K, 2)
+  return (u[:, :, 0] - left).reshape(batch * K)
 
 
 def sweep_pair(pkg, op, u0, dt, nsteps, t0=0.0):
@@ -92,7 +91,7 @@ def test_record_pair_equals_snapshot_pair(pkg, gpu, N, K, batch, tw, rtw, spl, n
   R = host(rec)
   for n in range(1, nsteps + 1):
     uin = oadv.inflow_value(op.a, t[n], inflow)
-    np.testing.assert_array_equal(R[n - 1], raw_jumps(host(snaps[n]), K, batch, N + 1, uin),
+    np.testing.assert_array_equal(R[n - 1, :K * batch], raw_jumps(host(snaps[n]), K, batch, N + 1, uin),
                                   err_msg=f"record {n - 1}")
   np.testing.assert_array_equal(host(w_r), host(w_s))
   np.testing.assert_array_equal(host(eta_r), host(eta_s))
@@ -120,8 +119,8 @@ def test_record_is_the_oracle_face_jumps(pkg, gpu):
     t += dt
     u = setup1d.from_elem_major(host(snaps[n]), N + 1)
     du = oadv.face_jumps(u, oadv.inflow_value(op.a, t, "a"), op.a, S)
-    du0 = 0.5 * (R[n - 1, :, 0] + R[n - 1, :, 1])
-    du1 = 0.5 * (R[n - 1, :, 1] - R[n - 1, :, 0])
+    du0 = R[n - 1, :K]
+    du1 = np.append(-R[n - 1, 1:K], 0.0)  # the right neighbour's left jump; outflow: 0
     np.testing.assert_allclose(du[0], -0.5 * op.a * du0, rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(du[1], 0.5 * op.a * du1, rtol=1e-12, atol=1e-12)
 
@@ -192,7 +191,7 @@ def test_record_rejects_what_it_cannot_do(pkg, gpu):
   lin = pkg.operators.DGAdvection1D(mesh)
   u = lin.new_field()
   lin.init_sine([1.0], [1.0], [0.0], out=u)
-  buf = torch.empty(2 * 2 * 100 + 1, dtype=torch.float64, device=gpu)
+  buf = torch.empty(2 * 100 + 1, dtype=torch.float64, device=gpu)
   with pytest.raises(pkg._lib.DGLibraryError):  # 8-byte aligned only
     lin.forward_rec(u, 0.0, 1e-4, 2, buf[1:])
   with pytest.raises(ValueError):
@@ -209,7 +208,7 @@ def rec_sweep(op, u0, dt, nsteps, t0=0.0):
   eta = torch.full((op.ktot,), float("nan"), dtype=torch.float64, device=op.device)
   op.adjoint_rec(w, rec, t0, dt, nsteps, eta=eta, eta_assign=True, eta_abs=True)
   torch.cuda.synchronize()
-  return host(rec), host(uN), host(w), host(eta)
+  return host(rec)[:, :op.ktot], host(uN), host(w), host(eta)  # (the pad entry is unwritten)
 
 
 @pytest.mark.parametrize("N,K,batch,rtw,spl,nsteps,inflow,refined", [
@@ -283,7 +282,8 @@ def test_pair_tiles_long_launches(pkg, gpu, N, K, batch, rtw, spl, nsteps):
   for n in range(1, nsteps + 1):
     uin = oadv.inflow_value(op.a, n * dt, "a")  # t_n by repeated addition: equal to rounding
     ref = raw_jumps(host(snaps[n]), K, batch, N + 1, uin)
-    np.testing.assert_allclose(rec[n - 1], ref, rtol=0, atol=1e-12 * scale, err_msg=f"record {n - 1}")
+    np.testing.assert_allclose(rec[n - 1, :K * batch], ref, rtol=0, atol=1e-12 * scale,
+                               err_msg=f"record {n - 1}")
   e_ref = np.abs(host(eta_s))
   np.testing.assert_allclose(eta, e_ref, rtol=0, atol=1e-7 * e_ref.max())
 
@@ -388,3 +388,36 @@ def test_env_override_is_the_tune_key(pkg, gpu, monkeypatch):
   monkeypatch.setenv("DG_REC_FWD_STEPS_PER_LAUNCH", "20")  # the forward's own override wins
   both = pkg.operators.DGAdvection1D(mesh)
   assert (both.rec_steps_per_launch, both.rec_fwd_steps_per_launch) == (8, 20)
+
+
+def test_forward_own_tile_width(pkg, gpu):
+  """The forward record sweep's own tile width (DG_TUNE_REC_FWD_TILE_WIDTH): the tile shape
+  never changes the arithmetic, so at equal steps per launch everything is bit-identical to
+  both directions on one width.  Np = 9's default is 1024-element tiles forward (one 20-step
+  launch) and 512-element tiles for the adjoint (10 steps); setting rec_tile_width applies to
+  both directions again."""
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=8, k=3000)
+  op = pkg.operators.DGAdvection1D(mesh, batch=2)
+  assert (op.rec_fwd_tile_width, op.rec_fwd_steps_per_launch) == (2, 20)
+  assert (op.rec_tile_width, op.rec_steps_per_launch, op.rec_lane_elements) == (1, 10, 2)
+  dt = mesh.cfl_dt()
+  u0 = op.new_field()
+  op.init_sine([1.0, 0.8], [2.0, 3.0], [0.0, 0.5], out=u0)
+  gen = torch.Generator(device=gpu).manual_seed(11)
+  u0 += 0.1 * torch.randn(u0.shape, dtype=u0.dtype, device=u0.device, generator=gen)
+  nsteps = 20
+  op.tune(rec_fwd_steps_per_launch=10)
+  mixed = rec_sweep(op, u0, dt, nsteps)
+  op.tune(rec_tile_width=2, rec_steps_per_launch=10)
+  assert (op.rec_fwd_tile_width, op.rec_tile_width) == (2, 2)
+  same = rec_sweep(op, u0, dt, nsteps)
+  for name, a, b in zip(("record", "u^N", "w^0", "eta"), mixed, same):
+    np.testing.assert_array_equal(a, b, err_msg=name)
+  op.tune(rec_fwd_tile_width=1)
+  assert (op.rec_fwd_tile_width, op.rec_tile_width) == (1, 2)
+  narrow = rec_sweep(op, u0, dt, nsteps)
+  for name, a, b in zip(("record", "u^N", "w^0", "eta"), narrow, same):
+    np.testing.assert_array_equal(a, b, err_msg=name)
+  with pytest.raises(pkg._lib.DGLibraryError):
+    op.tune(rec_fwd_tile_width=3)
