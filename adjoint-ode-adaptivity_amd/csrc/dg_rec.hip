@@ -146,28 +146,104 @@ __device__ __forceinline__ void rp_rec_get(const double* __restrict__ rec, int64
   }
 }
 
+// ---------------------------------------------------------------------------
+// The LSERK4 step as its stability polynomial, in Horner form (round 3).
+//
+// For the linear sweep du/dt = L u + (inflow at a trajectory's first element) the five
+// low-storage stages (utils/One_code.mlx:120-137, coefficients utils/Globals1D.m:19-34) are
+//   u^{n+1} = P(z) u^n + sum_{k<5} z^k zb b_k,    P(z) = sum_{k<=5} beta_k z^k,  z = dt L,
+// zb the lift of a left boundary value and b_k = sum_s g_{s,k} uin(t_n + c_s dt) (the stage
+// inflow values' weights, rk_poly below).  Evaluated as
+//   t = beta_4 u + beta_5 Z_{b_4/beta_5}(u);  t = beta_k u + Z_{b_k}(t), k = 3, 2, 1;
+//   u^{n+1} = u + Z_{b_0}(t),          Z_b(v) = z v + zb b  (b: the first element's uL)
+// it is still five applications of z -- five face exchanges per step -- but 125 fp64
+// operations per element-step at Np = 5 instead of the stage loop's 155 (no low-storage
+// carry A_s r, no B_s update), and the adjoint's P(z^T) w 135 instead of 170.  Equal to the
+// stage loop to rounding: 2e-16 relative per step (profiles/r03/horner_check.py; the oracle
+// keeps the stage loop).  beta_0 = beta_1 = 1 exactly in double (checked on the host), so the
+// last two levels take u itself as the accumulator's start.
+// ---------------------------------------------------------------------------
+struct RkPoly {
+  double beta[6];   // P(z) = sum_k beta_k z^k
+  double g[5][5];   // g[s][k]: weight of stage s's inflow value in b_k
+  bool ok;
+};
+
+// The polynomial coefficients from the stage recursion (r = A_s r + z u + zb uin_s;
+// u = u + B_s r) on coefficient vectors in z, in long double, rounded once.
+inline const RkPoly& rk_poly() {
+  static const RkPoly P = [] {
+    long double uc[6] = {1}, rc[6] = {0}, uf[5][6] = {}, rf[5][6] = {};
+    for (int s = 0; s < 5; ++s) {
+      const long double A = RK<5>::A(s), B = RK<5>::B(s);
+      for (int k = 5; k >= 0; --k) rc[k] = A * rc[k] + (k ? uc[k - 1] : 0.0L);
+      for (int q = 0; q < 5; ++q)
+        for (int k = 5; k >= 0; --k)
+          rf[q][k] = A * rf[q][k] + (k ? uf[q][k - 1] : 0.0L) + ((q == s && k == 0) ? 1.0L : 0.0L);
+      for (int k = 0; k < 6; ++k) uc[k] += B * rc[k];
+      for (int q = 0; q < 5; ++q)
+        for (int k = 0; k < 6; ++k) uf[q][k] += B * rf[q][k];
+    }
+    RkPoly r{};
+    for (int k = 0; k < 6; ++k) r.beta[k] = double(uc[k]);
+    for (int q = 0; q < 5; ++q)
+      for (int k = 0; k < 5; ++k) r.g[q][k] = double(uf[q][k]);
+    r.ok = r.beta[0] == 1.0 && r.beta[1] == 1.0 && r.beta[5] != 0.0;
+    return r;
+  }();
+  return P;
+}
+
+// Arguments of a forward launch of MS steps.
+template <int NP, int MS> struct RpStepArgs {
+  EOArgs<NP> op;
+  double sc;                    // dt (non-uniform meshes multiply by scale[k]; uniform: in op)
+  double beta[6];               // P's coefficients
+  double bnd[MS * 5 + MS + 1];  // step st, level l = 0..4: bnd[5 st + l] = b_4/beta_5, b_3,
+                                // b_2, b_1, b_0; then bnd[5 MS + st] = uin(t_{n0+st}), the
+                                // record's inflow value, st = 0..MS
+  int64_t ktot;
+  int64_t n0;                   // global index of the launch's first step
+  int32_t K;
+  int32_t xcd;
+  int32_t jend;                 // the launch ends the sweep (record u^{n0+MS} too)
+};
+
+template <int NP, int MS> struct RpAdjArgs {
+  EOArgs<NP> op;
+  double sc;
+  double beta[6];
+  int64_t ktot;
+  int64_t n0;
+  int32_t K;
+  int32_t has_eta;  // kEta* bits
+  int32_t xcd;
+};
+
 template <int NP, bool UNI, int NW, int E, int MS>
 __global__ __launch_bounds__(64 * NW) void k_step_rp(const double* __restrict__ uin,
                                                         double* __restrict__ rec,
                                                         double* __restrict__ last,
                                                         const double* __restrict__ scale,
-                                                        StepArgs<NP, 5, MS> args);
+                                                        RpStepArgs<NP, MS> args);
 
-// Forward: MS LSERK4 steps of the tile; records u^{n0}..u^{n0+MS-1}'s jumps (and u^{n0+MS}'s
-// when the launch ends the sweep), writes u^{n0+MS} to `last`.  See step_tile (dg_advec.hip).
+// Forward: MS steps of the tile; records u^{n0}..u^{n0+MS-1}'s jumps (and u^{n0+MS}'s when
+// the launch ends the sweep), writes u^{n0+MS} to `last`.  Per step five Horner levels, each
+// one face exchange of its input vector v (u at level 0, t after) through LDS.
 template <int NP, bool UNI, int NW, int E, int MS, bool EDGE>
 __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t tile,
                                              const double* __restrict__ uin,
                                              double* __restrict__ rec, double* __restrict__ last,
                                              const double* __restrict__ scale,
-                                             const StepArgs<NP, 5, MS>& args) {
+                                             const RpStepArgs<NP, MS>& args) {
   using G = RpGeo<NP, NW, E>;
-  constexpr int NS = 5, T = G::T, LB = G::LB;
-  constexpr int H = RpHalo<MS>::F;  // the stage cone + the final state's neighbours, even
+  constexpr int T = G::T, LB = G::LB;
+  constexpr int H = RpHalo<MS>::F;  // the level cone + the final state's neighbours, even
   constexpr int TE = T - 2 * H;
   static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && E == 2, "pair tiles: aligned pairs");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
-  constexpr int CB = G::kLds;  // lds[CB + st*NS + s] = inflow value of that stage
+  constexpr int CB = G::kLds;  // lds[CB + i] = args.bnd[i] (edge tiles)
+  constexpr int CR = CB + MS * 5;  // the record's inflow values
   constexpr int FB = LB + 2;   // one face array
   const int lane = threadIdx.x;
   const int64_t e0 = tile * TE - H;
@@ -175,65 +251,88 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
 
   const int off = rp_load<NP, NW, E, EDGE>(uin, e0, nd, lds);
   if constexpr (EDGE) {
-    using SArgs = StepArgs<NP, NS, MS>;  // lane-indexed kernarg read, see step_tile
+    using SArgs = RpStepArgs<NP, MS>;  // lane-indexed kernarg read, see step_tile
     const double* ka = reinterpret_cast<const double*>(
-        kernarg_tail<decltype(&k_step_rp<NP, UNI, NW, E, MS>), SArgs>() + offsetof(SArgs, uin));
-    if (lane <= MS * NS) lds[CB + lane] = ka[lane];
+        kernarg_tail<decltype(&k_step_rp<NP, UNI, NW, E, MS>), SArgs>() + offsetof(SArgs, bnd));
+    if (lane <= MS * 6) lds[CB + lane] = ka[lane];
   }
   __syncthreads();
-  double ev[E][NE], od[E][NO];
+  double ue[E][NE], uo[E][NO];  // u in even/odd coordinates
   Elem El[E];
   double sc[E], jv[E];
 #pragma unroll
   for (int m = 0; m < E; ++m) {
     const int el = E * lane + m;
     const double* us = lds + off + el * NP;
-    to_eo<NP>(us, ev[m], od[m]);
+    to_eo<NP>(us, ue[m], uo[m]);
     El[m] = elem_info<H, T, EDGE>(e0, el, args.ktot, args.K);
     sc[m] = args.sc;
     if constexpr (!UNI) sc[m] *= El[m].inrange ? scale[El[m].kl] : 0.0;
     // u^{n0}'s left-face jumps (record n0-1) from the staged nodal values, as step_tile
-    jv[m] = us[0] - ((EDGE && El[m].first) ? lds[CB] : us[-1]);
+    jv[m] = us[0] - ((EDGE && El[m].first) ? lds[CR] : us[-1]);
   }
   if (args.n0 >= 1) rp_rec_put<EDGE>(rec, args.n0 - 1, args.ktot, El, jv[0], jv[1]);
   __syncthreads();  // the image is read: the face arrays alias it
 
-  double re[E][NE], ro[E][NO];
-  // The step loop stays rolled (8x less code than unrolled, measured equal or faster); the
-  // stage loop inside is unrolled, so the RK coefficients are immediates.
+  const double b4 = args.beta[4], b5 = args.beta[5], b3 = args.beta[3], b2 = args.beta[2];
+  double te[E][NE], to[E][NO];  // the Horner accumulator t
+  // The step loop stays rolled; the level loop inside is unrolled.
 #pragma unroll 1
   for (int st = 0; st < MS; ++st) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int fL = ((st * NS + s) & 1) * 2 * FB;  // buffers alternate over the global stage
+    for (int l = 0; l < 5; ++l) {
+      const int fL = ((st * 5 + l) & 1) * 2 * FB;  // buffers alternate over the global level
       const int fR = fL + FB;
-      double u0[E], uN[E];
+      // the level's input v: u at level 0, t after
+      double v0[E], vN[E];
 #pragma unroll
       for (int m = 0; m < E; ++m) {
-        u0[m] = ev[m][0] + od[m][0];
-        uN[m] = ev[m][0] - od[m][0];
+        const double e = (l == 0) ? ue[m][0] : te[m][0], o = (l == 0) ? uo[m][0] : to[m][0];
+        v0[m] = e + o;
+        vN[m] = e - o;
       }
-      lds[fL + lane + 1] = u0[0];      // the lane's left face
-      lds[fR + lane + 1] = uN[E - 1];  // the lane's right face
+      lds[fL + lane + 1] = v0[0];      // the lane's left face
+      lds[fR + lane + 1] = vN[E - 1];  // the lane's right face
       __builtin_amdgcn_sched_barrier(0);
+      // Volume part, before the barrier: pe = c u + Qeo vo, po = c u + Qoe ve on uniform
+      // meshes (c = beta_{4-l}; level 0 has no u term here, c = 1 from level 3 on), the bare
+      // products on non-uniform ones (the metric multiplies them after the lift).
       double pe[E][NE], po[E][NO];
 #pragma unroll
       for (int m = 0; m < E; ++m) {
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
-          double t = (UNI && s > 0) ? RK<NS>::A(s) * re[m][k] : args.op.Qeo[k * NO] * od[m][0];
+          const double* vo = (l == 0) ? uo[m] : to[m];
+          double a;
+          int j0 = 0;
+          if (UNI && l >= 3) {
+            a = ue[m][k];
+          } else if (UNI && l >= 1) {
+            a = (l == 1 ? b3 : b2) * ue[m][k];
+          } else {
+            a = args.op.Qeo[k * NO] * vo[0];
+            j0 = 1;
+          }
 #pragma unroll
-          for (int j = (UNI && s > 0) ? 0 : 1; j < NO; ++j)
-            t = fma(args.op.Qeo[k * NO + j], od[m][j], t);
-          pe[m][k] = t;
+          for (int j = j0; j < NO; ++j) a = fma(args.op.Qeo[k * NO + j], vo[j], a);
+          pe[m][k] = a;
         }
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
-          double t = (UNI && s > 0) ? RK<NS>::A(s) * ro[m][k] : args.op.Qoe[k * NE] * ev[m][0];
+          const double* ve = (l == 0) ? ue[m] : te[m];
+          double a;
+          int j0 = 0;
+          if (UNI && l >= 3) {
+            a = uo[m][k];
+          } else if (UNI && l >= 1) {
+            a = (l == 1 ? b3 : b2) * uo[m][k];
+          } else {
+            a = args.op.Qoe[k * NE] * ve[0];
+            j0 = 1;
+          }
 #pragma unroll
-          for (int j = (UNI && s > 0) ? 0 : 1; j < NE; ++j)
-            t = fma(args.op.Qoe[k * NE + j], ev[m][j], t);
-          po[m][k] = t;
+          for (int j = j0; j < NE; ++j) a = fma(args.op.Qoe[k * NE + j], ve[j], a);
+          po[m][k] = a;
         }
 #pragma unroll
         for (int k = 0; k < NE; ++k) pin(pe[m][k]);
@@ -243,51 +342,62 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
       __syncthreads();
       // lane-1's right face / lane+1's left face (the pads feed halo elements only)
       const double fromL = lds[fR + lane], fromR = lds[fL + lane + 2];
-      double uin_s = 0.0;
-      if constexpr (EDGE) uin_s = lds[CB + st * NS + s];
+      double bnd = 0.0, urec = 0.0;
+      if constexpr (EDGE) {
+        bnd = lds[CB + st * 5 + l];
+        if (l == 0) urec = lds[CR + st];
+      }
 #pragma unroll
       for (int m = 0; m < E; ++m) {
-        double uL = (m == 0) ? fromL : uN[m - 1];
-        double uR = (m == E - 1) ? fromR : u0[m + 1];
+        double vL = (m == 0) ? fromL : vN[m - 1];
+        double vR = (m == E - 1) ? fromR : v0[m + 1];
+        if (l == 0) jv[m] = v0[m] - ((EDGE && El[m].first) ? urec : vL);  // u^{n0+st}'s jump
         if constexpr (EDGE) {
-          uL = El[m].first ? uin_s : uL;
-          uR = El[m].last ? uN[m] : uR;
+          vL = El[m].first ? bnd : vL;
+          vR = El[m].last ? vN[m] : vR;
         }
-        const double dlt = uR - uL, sig = -(uL + uR);
-        if (s == 0) jv[m] = u0[m] - uL;  // u^{n0+st}'s left-face jump
+        const double dlt = vR - vL, sig = -(vL + vR);
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
+          const double z = fma(args.op.le[k], dlt, pe[m][k]);
           if constexpr (UNI) {
-            re[m][k] = fma(args.op.le[k], dlt, pe[m][k]);
+            if (l == 0) te[m][k] = fma(b5, z, b4 * ue[m][k]);
+            else if (l < 4) te[m][k] = z;
+            else ue[m][k] = z;
           } else {
-            const double a = sc[m] * fma(args.op.le[k], dlt, pe[m][k]);
-            re[m][k] = (s == 0) ? a : fma(RK<NS>::A(s), re[m][k], a);
+            if (l == 0) te[m][k] = fma(b5 * sc[m], z, b4 * ue[m][k]);
+            else if (l < 3) te[m][k] = fma(sc[m], z, (l == 1 ? b3 : b2) * ue[m][k]);
+            else if (l == 3) te[m][k] = fma(sc[m], z, ue[m][k]);
+            else ue[m][k] = fma(sc[m], z, ue[m][k]);
           }
-          ev[m][k] = fma(RK<NS>::B(s), re[m][k], ev[m][k]);
         }
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
+          const double z = fma(args.op.lo[k], sig, po[m][k]);
           if constexpr (UNI) {
-            ro[m][k] = fma(args.op.lo[k], sig, po[m][k]);
+            if (l == 0) to[m][k] = fma(b5, z, b4 * uo[m][k]);
+            else if (l < 4) to[m][k] = z;
+            else uo[m][k] = z;
           } else {
-            const double a = sc[m] * fma(args.op.lo[k], sig, po[m][k]);
-            ro[m][k] = (s == 0) ? a : fma(RK<NS>::A(s), ro[m][k], a);
+            if (l == 0) to[m][k] = fma(b5 * sc[m], z, b4 * uo[m][k]);
+            else if (l < 3) to[m][k] = fma(sc[m], z, (l == 1 ? b3 : b2) * uo[m][k]);
+            else if (l == 3) to[m][k] = fma(sc[m], z, uo[m][k]);
+            else uo[m][k] = fma(sc[m], z, uo[m][k]);
           }
-          od[m][k] = fma(RK<NS>::B(s), ro[m][k], od[m][k]);
         }
       }
-      if (s == 0 && st >= 1) rp_rec_put<EDGE>(rec, args.n0 + st - 1, args.ktot, El, jv[0], jv[1]);
+      if (l == 0 && st >= 1) rp_rec_put<EDGE>(rec, args.n0 + st - 1, args.ktot, El, jv[0], jv[1]);
     }
   }
   if (args.jend) {
     // the sweep's final state u^{n0+MS}: one more face exchange for its jumps (record
     // n0+MS-1), inflow at t_{n0+MS}
-    const int fL = ((MS * NS) & 1) * 2 * FB, fR = fL + FB;
+    const int fL = ((MS * 5) & 1) * 2 * FB, fR = fL + FB;
     double u0[E], uN[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-      u0[m] = ev[m][0] + od[m][0];
-      uN[m] = ev[m][0] - od[m][0];
+      u0[m] = ue[m][0] + uo[m][0];
+      uN[m] = ue[m][0] - uo[m][0];
     }
     lds[fL + lane + 1] = u0[0];
     lds[fR + lane + 1] = uN[E - 1];
@@ -296,13 +406,13 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
 #pragma unroll
     for (int m = 0; m < E; ++m) {
       double uL = (m == 0) ? fromL : uN[m - 1];
-      if constexpr (EDGE) uL = El[m].first ? lds[CB + MS * NS] : uL;
+      if constexpr (EDGE) uL = El[m].first ? lds[CR + MS] : uL;
       jv[m] = u0[m] - uL;
     }
     rp_rec_put<EDGE>(rec, args.n0 + MS - 1, args.ktot, El, jv[0], jv[1]);
   }
   __syncthreads();  // the last face reads are done: the image is rewritten
-  rp_store<NP, NW, E, H, EDGE>(last, tile * TE * NP, nd, lds, ev, od, false);
+  rp_store<NP, NW, E, H, EDGE>(last, tile * TE * NP, nd, lds, ue, uo, false);
 }
 
 template <int NP, bool UNI, int NW, int E, int MS>
@@ -310,9 +420,9 @@ __global__ __launch_bounds__(64 * NW) void k_step_rp(const double* __restrict__ 
                                                         double* __restrict__ rec,
                                                         double* __restrict__ last,
                                                         const double* __restrict__ scale,
-                                                        StepArgs<NP, 5, MS> args) {
+                                                        RpStepArgs<NP, MS> args) {
   using G = RpGeo<NP, NW, E>;
-  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 6 + 1];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
   constexpr int H = RpHalo<MS>::F;
   const int64_t e0 = tile * (G::T - 2 * H) - H;
@@ -323,8 +433,11 @@ __global__ __launch_bounds__(64 * NW) void k_step_rp(const double* __restrict__ 
 }
 
 // Adjoint: MS reverse steps st = MS-1..0 of the tile, each
-//   eta += DWR(u^{n0+st+1}'s recorded jumps, w^{n0+st+1});  w^{n0+st} = S^T w^{n0+st+1}
-// (terminal functionals only: no source).  See adj_tile (dg_advec.hip).
+//   eta += DWR(u^{n0+st+1}'s recorded jumps, w^{n0+st+1});  w^{n0+st} = P(z^T) w^{n0+st+1}
+// (terminal functionals only: no source; the inflow forcing does not depend on u).  Horner
+// in z^T: t = beta_4 w + beta_5 z^T w; t = beta_k w + z^T t, k = 3, 2, 1; w = w + z^T t, with
+// z^T v = L^T (sc v): the face adjoints g0 = le.ve + lo.vo, g1 = lo.vo - le.ve of each element
+// go to its neighbours (one exchange per level), the transposed volume blocks stay local.
 template <int NP, bool UNI, int NW, int E, int MS, bool EDGE>
 __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t tile,
                                             const double* __restrict__ win,
@@ -332,9 +445,9 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
                                             const double* __restrict__ rec,
                                             double* __restrict__ eta,
                                             const double* __restrict__ scale,
-                                            const AdjArgs<NP, MS>& args) {
+                                            const RpAdjArgs<NP, MS>& args) {
   using G = RpGeo<NP, NW, E>;
-  constexpr int NS = 5, T = G::T, LB = G::LB;
+  constexpr int T = G::T, LB = G::LB;
   constexpr int H = RpHalo<MS>::A;
   constexpr int TE = T - 2 * H;
   static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && E == 2, "pair tiles: aligned pairs");
@@ -372,12 +485,14 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
   }
   __syncthreads();  // the image is read: the face arrays alias it
 
+  const double b4 = args.beta[4], b5 = args.beta[5], b3 = args.beta[3], b2 = args.beta[2];
+  double te[E][NE], to[E][NO];  // the Horner accumulator
 #pragma unroll 1
   for (int st = MS - 1; st >= 0; --st) {
     // du0 = j_e; du1 = -j_{e+1} (0 at a trajectory's last element): du0 - du1 and du0 + du1
-    // are the snapshot path's doubles bit for bit (dg_common.h rec_ld)
+    // are the snapshot path's doubles bit for bit (dg_common.h rec_ld).  The next step's
+    // record is loaded after this step's indicator has read the current one.
     const double jc[E + 1] = {jn.x, jn.y, jn2};
-    if (st > 0) rp_rec_get<EDGE>(rec, args.n0 + st - 1, args.ktot, ea, jn, jn2);
     if (args.has_eta) {
 #pragma unroll
       for (int m = 0; m < E; ++m) {
@@ -394,34 +509,27 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
         eacc[m] += c;
       }
     }
-    double le_[E][NE], lo_[E][NO];
+    if (st > 0) rp_rec_get<EDGE>(rec, args.n0 + st - 1, args.ktot, ea, jn, jn2);
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-#pragma unroll
-      for (int k = 0; k < NE; ++k) le_[m][k] = 0.0;
-#pragma unroll
-      for (int k = 0; k < NO; ++k) lo_[m][k] = 0.0;
-    }
-#pragma unroll
-    for (int ss = 0; ss < NS; ++ss) {
-      const int s = NS - 1 - ss;
-      // buffers alternate over the launch's global reverse-stage index (no barrier between
-      // a step's last stage and the next step's first)
-      const int f0 = (((MS - 1 - st) * NS + ss) & 1) * 2 * FB, f1 = f0 + FB;
+    for (int l = 0; l < 5; ++l) {
+      // buffers alternate over the launch's global level index (no barrier between a step's
+      // last level and the next step's first)
+      const int f0 = (((MS - 1 - st) * 5 + l) & 1) * 2 * FB, f1 = f0 + FB;
+      // the level's input v (w at level 0, t after), scaled by the metric: q = sc v
       double g0[E], g1[E], qe[E][NE], qo[E][NO];
 #pragma unroll
       for (int m = 0; m < E; ++m) {
         double gd = 0.0, gs = 0.0;
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
-          le_[m][k] = fma(RK<NS>::B(s), we[m][k], le_[m][k]);
-          qe[m][k] = UNI ? le_[m][k] : sc[m] * le_[m][k];
+          const double v = (l == 0) ? we[m][k] : te[m][k];
+          qe[m][k] = UNI ? v : sc[m] * v;
           gd = fma(args.op.le[k], qe[m][k], gd);
         }
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
-          lo_[m][k] = fma(RK<NS>::B(s), wo[m][k], lo_[m][k]);
-          qo[m][k] = UNI ? lo_[m][k] : sc[m] * lo_[m][k];
+          const double v = (l == 0) ? wo[m][k] : to[m][k];
+          qo[m][k] = UNI ? v : sc[m] * v;
           gs = fma(args.op.lo[k], qo[m][k], gs);
         }
         g0[m] = gd + gs;
@@ -430,31 +538,47 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
       lds[f0 + lane + 1] = g0[0];      // the lane's first element: adjoint of its uL
       lds[f1 + lane + 1] = g1[E - 1];  // the lane's last element: adjoint of its uR
       __builtin_amdgcn_sched_barrier(0);
+      // the transposed volume term, before the barrier: a = c w + Qoe^T qo (even), c w +
+      // Qeo^T qe (odd); level 0 starts from the bare products
+      double ae[E][NE], ao[E][NO];
 #pragma unroll
       for (int m = 0; m < E; ++m) {
-        // the transposed volume term and the carry need no neighbour data
 #pragma unroll
         for (int j = 0; j < NE; ++j) {
-          double t = we[m][j];
+          double t;
+          int k0 = 0;
+          if (l >= 3) {
+            t = we[m][j];
+          } else if (l >= 1) {
+            t = (l == 1 ? b3 : b2) * we[m][j];
+          } else {
+            t = args.op.Qoe[j] * qo[m][0];
+            k0 = 1;
+          }
 #pragma unroll
-          for (int k = 0; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[m][k], t);
-          we[m][j] = t;
+          for (int k = k0; k < NO; ++k) t = fma(args.op.Qoe[k * NE + j], qo[m][k], t);
+          ae[m][j] = t;
         }
 #pragma unroll
         for (int j = 0; j < NO; ++j) {
-          double t = wo[m][j];
+          double t;
+          int k0 = 0;
+          if (l >= 3) {
+            t = wo[m][j];
+          } else if (l >= 1) {
+            t = (l == 1 ? b3 : b2) * wo[m][j];
+          } else {
+            t = args.op.Qeo[j] * qe[m][0];
+            k0 = 1;
+          }
 #pragma unroll
-          for (int k = 0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[m][k], t);
-          wo[m][j] = t;
+          for (int k = k0; k < NE; ++k) t = fma(args.op.Qeo[k * NO + j], qe[m][k], t);
+          ao[m][j] = t;
         }
 #pragma unroll
-        for (int k = 0; k < NE; ++k) le_[m][k] = RK<NS>::A(s) * le_[m][k];
+        for (int k = 0; k < NE; ++k) pin(ae[m][k]);
 #pragma unroll
-        for (int k = 0; k < NO; ++k) lo_[m][k] = RK<NS>::A(s) * lo_[m][k];
-#pragma unroll
-        for (int k = 0; k < NE; ++k) pin(we[m][k]);
-#pragma unroll
-        for (int k = 0; k < NO; ++k) pin(wo[m][k]);
+        for (int k = 0; k < NO; ++k) pin(ao[m][k]);
       }
       __syncthreads();
       // lane-1's last element's g1 / lane+1's first element's g0
@@ -469,8 +593,20 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
           gl = El[m].first ? 0.0 : gl;
           gr = El[m].last ? g1[m] : gr;
         }
-        we[m][0] -= gl + gr;
-        wo[m][0] += gr - gl;
+        ae[m][0] -= gl + gr;
+        ao[m][0] += gr - gl;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          if (l == 0) te[m][k] = fma(b5, ae[m][k], b4 * we[m][k]);
+          else if (l < 4) te[m][k] = ae[m][k];
+          else we[m][k] = ae[m][k];
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          if (l == 0) to[m][k] = fma(b5, ao[m][k], b4 * wo[m][k]);
+          else if (l < 4) to[m][k] = ao[m][k];
+          else wo[m][k] = ao[m][k];
+        }
       }
     }
   }
@@ -487,7 +623,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_rp(const double* __restrict__ w
                                                        const double* __restrict__ rec,
                                                        double* __restrict__ eta,
                                                        const double* __restrict__ scale,
-                                                       AdjArgs<NP, MS> args) {
+                                                       RpAdjArgs<NP, MS> args) {
   using G = RpGeo<NP, NW, E>;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
@@ -502,14 +638,25 @@ __global__ __launch_bounds__(64 * NW) void k_adj_rp(const double* __restrict__ w
 template <int NP, int NW, int E, int MS>
 int rp_step_e(const dg_plan* p, const double* in, double* rec, double* last, const double* times,
               double dt, hipStream_t st, int64_t n0, bool jend) {
-  StepArgs<NP, 5, MS> a;
+  const RkPoly& P = rk_poly();
+  if (!P.ok) return fail(DG_ERR_HIP, "LSERK4 stability polynomial: beta_0 = beta_1 = 1 expected");
+  RpStepArgs<NP, MS> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
   a.sc = dt;
-  for (int m = 0; m < MS; ++m)
-    for (int s = 0; s < 5; ++s) a.uin[m * 5 + s] = inflow_value(p, times[m] + RK<5>::C(s) * dt);
-  a.uin[MS * 5] = inflow_value(p, times[MS]);
+  for (int k = 0; k < 6; ++k) a.beta[k] = P.beta[k];
+  for (int m = 0; m < MS; ++m) {
+    double u[5], b[5];
+    for (int s = 0; s < 5; ++s) u[s] = inflow_value(p, times[m] + RK<5>::C(s) * dt);
+    for (int k = 0; k < 5; ++k) {
+      double acc = 0.0;
+      for (int s = 0; s < 5; ++s) acc = std::fma(P.g[s][k], u[s], acc);
+      b[k] = acc;
+    }
+    a.bnd[m * 5 + 0] = b[4] / P.beta[5];
+    for (int l = 1; l < 5; ++l) a.bnd[m * 5 + l] = b[4 - l];
+  }
+  for (int m = 0; m <= MS; ++m) a.bnd[MS * 5 + m] = inflow_value(p, times[m]);
   a.ktot = p->ktot;
-  a.stride = p->ktot * NP;
   a.n0 = n0;
   a.K = int32_t(p->K);
   a.xcd = p->xcd_order;
@@ -528,16 +675,14 @@ int rp_step_e(const dg_plan* p, const double* in, double* rec, double* last, con
 
 template <int NP, int NW, int E, int MS>
 int rp_adj_e(const dg_plan* p, const double* win, double* wout, const double* rec, double* eta,
-             int eta_mode, const double* t_next, double dt, hipStream_t st, int64_t n0) {
-  AdjArgs<NP, MS> a;
+             int eta_mode, const double* /*t_next*/, double dt, hipStream_t st, int64_t n0) {
+  const RkPoly& P = rk_poly();
+  if (!P.ok) return fail(DG_ERR_HIP, "LSERK4 stability polynomial: beta_0 = beta_1 = 1 expected");
+  RpAdjArgs<NP, MS> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : 1.0, &a.op, true);
   a.sc = dt;
-  for (int m = 0; m < MS; ++m) {
-    a.uin_res[m] = inflow_value(p, t_next[m]);
-    a.src[m] = 0.0;
-  }
+  for (int k = 0; k < 6; ++k) a.beta[k] = P.beta[k];
   a.ktot = p->ktot;
-  a.stride = p->ktot * NP;
   a.n0 = n0;
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr ? (eta_mode | kEtaOn) : 0;

@@ -84,7 +84,7 @@ def halo_factor(T, H):
   """Lanes issued per useful lane of a tile of T elements whose launch writes T - 2 H."""
   return T / float(T - 2 * H)
 PROFILE_TRAFFIC = {  # per-launch PMC traffic of the sweep kernels (profiles/r02/collect.sh)
-    "jumps": os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
+    "jumps": os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
     "snapshots": os.path.join(ROOT, "profiles", "r02", "pmc_traffic_snapshots.json")}
 
 

@@ -28,8 +28,11 @@ def main():
   p.add_argument("--nsteps", type=int, default=20)
   p.add_argument("--rounds", type=int, default=7)
   p.add_argument("--variants", default="20:10,10:10,20:20")
+  p.add_argument("--lib", default=None, help="load this libdgadv.so instead (experiment builds)")
   a = p.parse_args()
   pkg = importlib.import_module("adjoint-ode-adaptivity_amd")
+  if a.lib:
+    pkg._lib.LIB_PATH = os.path.abspath(a.lib)
   mesh = pkg.BaseGalerkin1D(n=a.N, k=a.K)
   op = pkg.operators.DGAdvection1D(mesh, batch=a.batch)
   dt = mesh.cfl_dt()
@@ -74,7 +77,7 @@ def main():
                                   "sweep_us": round(f + d, 2),
                                   "dof_updates_per_s": dof / (f + d) * 1e6,
                                   "bit_identical_to_first_same_steps": same.get(v, True)}
-  print(json.dumps({"N": a.N, "K": a.K, "batch": a.batch, "nsteps": a.nsteps,
+  print(json.dumps({"N": a.N, "K": a.K, "batch": a.batch, "nsteps": a.nsteps, "lib": a.lib,
                     "variant": "fwd_steps:adj_steps[:tile_width]", "results": out},
                    indent=1))
 

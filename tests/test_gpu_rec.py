@@ -9,9 +9,15 @@ Bars:
   * the record equals the jumps of the snapshot sweep's states, bit for bit (same doubles,
     same subtractions), and agrees with the oracle's AdvecRHS1D face jumps (face_jumps,
     which carry the (a nx)/2 factors) to rounding;
-  * final state, w^0 and eta equal the snapshot sweep pair's (src_coef = 0) bit for bit,
-    for every tile shape, steps per launch, batch (trajectory edges inside tiles), inflow
-    variant and a refined (non-uniform) mesh.
+  * with one element per lane (the stage-loop record kernels of dg_advec.hip) final state,
+    w^0 and eta equal the snapshot sweep pair's (src_coef = 0) bit for bit, for every tile
+    shape, steps per launch, batch (trajectory edges inside tiles), inflow variant and a
+    refined (non-uniform) mesh;
+  * the pair-tile kernels (dg_rec.hip, the default) evaluate each LSERK4 step as its stability
+    polynomial in Horner form (round 3): equal to the stage loop to rounding, so against the
+    snapshot pair they are held to HORNER_RTOL of max|.| on ICs with resolved jumps (a smooth
+    IC's jumps are below fp64 resolution at fine meshes and its indicator is rounding noise),
+    and bit for bit across their own tile shapes.
 """
 import numpy as np
 import pytest
@@ -22,8 +28,29 @@ from oracle import setup1d
 pytestmark = pytest.mark.gpu
 
 
+HORNER_RTOL = 1e-11  # Horner vs stage loop: ~2e-16 per step; the parity bar is 1e-10
+
+
 def host(t):
   return t.detach().cpu().numpy()
+
+
+def close(a, b, rtol=HORNER_RTOL, what=""):
+  a, b = np.asarray(a), np.asarray(b)
+  np.testing.assert_allclose(a, b, rtol=0, atol=rtol * max(np.abs(b).max(), 1e-300), err_msg=what)
+
+
+def noisy_sine(op, seed, batch):
+  """Sine ICs plus seeded per-node noise of 0.1: O(0.1) interelement jumps, a well-conditioned
+  indicator."""
+  import torch
+  rng = np.random.default_rng(seed)
+  u0 = op.new_field()
+  op.init_sine(rng.uniform(0.5, 1.5, batch), rng.integers(1, 5, batch).astype(float),
+               rng.uniform(0, 6, batch), out=u0)
+  gen = torch.Generator(device=u0.device).manual_seed(seed)
+  u0 += 0.1 * torch.randn(u0.shape, dtype=u0.dtype, device=u0.device, generator=gen)
+  return u0
 
 
 def raw_jumps(u_em, K, batch, Np, uin):
@@ -66,35 +93,42 @@ def sweep_pair(pkg, op, u0, dt, nsteps, t0=0.0):
     (8, 400, 1, 2, 2, 2, 7, "a"),
     (4, 77, 1, 1, 1, 4, 2, "a"),     # one launch, fewer steps than steps_per_launch
 ])
-def test_record_pair_equals_snapshot_pair(pkg, gpu, N, K, batch, tw, rtw, spl, nsteps, inflow):
+@pytest.mark.parametrize("lane_elements", [1, 2])
+def test_record_pair_equals_snapshot_pair(pkg, gpu, N, K, batch, tw, rtw, spl, nsteps, inflow,
+                                          lane_elements):
   """At equal steps per launch (which sets where the state leaves even/odd coordinates);
-  tile widths never change the arithmetic."""
-  import torch
+  tile widths never change the arithmetic.  One element per lane: bit for bit; pair tiles
+  (Horner form): to HORNER_RTOL."""
   mesh = pkg.BaseGalerkin1D(n=N, k=K)
   op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
   op.tune(tile_width=tw, steps_per_launch=spl, lane_elements=0, rec_tile_width=rtw,
-          rec_steps_per_launch=spl)
+          rec_steps_per_launch=spl, rec_lane_elements=lane_elements)
   assert op.rec_steps_per_launch == op.steps_per_launch
   dt = mesh.cfl_dt()
-  u0 = op.new_field()
-  rng = np.random.default_rng(N * 100 + K)
-  op.init_sine(rng.uniform(0.5, 1.5, batch), rng.integers(1, 5, batch).astype(float),
-               rng.uniform(0, 6, batch), out=u0)
+  u0 = noisy_sine(op, N * 100 + K, batch)
   u0_copy = u0.clone()
   snaps, w_s, eta_s, rec, uN, w_r, eta_r = sweep_pair(pkg, op, u0, dt, nsteps, t0=0.01)
   np.testing.assert_array_equal(host(u0), host(u0_copy))  # u0 untouched
-  np.testing.assert_array_equal(host(uN), host(snaps[nsteps]))
-  # the record: u^n's jumps at t_n, n = 1..nsteps
+  exact = lane_elements == 1
+  same = np.testing.assert_array_equal if exact else (lambda a, b, err_msg="": close(a, b, what=err_msg))
+  same(host(uN), host(snaps[nsteps]), err_msg="u^N")
+  # the record: u^n's jumps at t_n, n = 1..nsteps (absolute error against max|u|: jumps are
+  # differences of O(1) values)
   t = [0.01]
   for _ in range(nsteps):
     t.append(t[-1] + dt)
   R = host(rec)
+  umax = np.abs(host(u0)).max()
   for n in range(1, nsteps + 1):
     uin = oadv.inflow_value(op.a, t[n], inflow)
-    np.testing.assert_array_equal(R[n - 1, :K * batch], raw_jumps(host(snaps[n]), K, batch, N + 1, uin),
-                                  err_msg=f"record {n - 1}")
-  np.testing.assert_array_equal(host(w_r), host(w_s))
-  np.testing.assert_array_equal(host(eta_r), host(eta_s))
+    ref = raw_jumps(host(snaps[n]), K, batch, N + 1, uin)
+    if exact:
+      np.testing.assert_array_equal(R[n - 1, :K * batch], ref, err_msg=f"record {n - 1}")
+    else:
+      np.testing.assert_allclose(R[n - 1, :K * batch], ref, rtol=0, atol=HORNER_RTOL * umax,
+                                 err_msg=f"record {n - 1}")
+  same(host(w_r), host(w_s), err_msg="w^0")
+  same(host(eta_r), host(eta_s), err_msg="eta")
   assert np.abs(host(eta_s)).max() > 0
 
 
@@ -125,23 +159,27 @@ def test_record_is_the_oracle_face_jumps(pkg, gpu):
     np.testing.assert_allclose(du[1], 0.5 * op.a * du1, rtol=1e-12, atol=1e-12)
 
 
-def test_record_pair_on_a_refined_mesh(pkg, gpu):
-  """Non-uniform metric (the refine loop's meshes): still bit-identical to the snapshots."""
+@pytest.mark.parametrize("lane_elements", [1, 2])
+def test_record_pair_on_a_refined_mesh(pkg, gpu, lane_elements):
+  """Non-uniform metric (the refine loop's meshes): bit-identical to the snapshots with one
+  element per lane, to HORNER_RTOL on pair tiles (their non-uniform Horner levels)."""
   N, K, nsteps = 4, 500, 8
   v_x = np.linspace(0.0, 1.0, K + 1)
   for k in (3, 170, 171, 499):
     v_x = np.insert(v_x, k + 1, 0.5 * (v_x[k] + v_x[k + 1]))
   mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
   op = pkg.operators.DGAdvection1D(mesh, batch=2)
-  op.tune(rec_tile_width=1, rec_steps_per_launch=op.steps_per_launch)
+  op.tune(rec_tile_width=1, rec_steps_per_launch=op.steps_per_launch,
+          rec_lane_elements=lane_elements)
   assert not op.uniform
   dt = mesh.cfl_dt()
-  u0 = op.new_field()
-  op.init_sine([1.0, 0.7], [2.0, 3.0], [0.0, 1.0], out=u0)
+  u0 = noisy_sine(op, 5, 2)
   snaps, w_s, eta_s, rec, uN, w_r, eta_r = sweep_pair(pkg, op, u0, dt, nsteps)
-  np.testing.assert_array_equal(host(uN), host(snaps[nsteps]))
-  np.testing.assert_array_equal(host(w_r), host(w_s))
-  np.testing.assert_array_equal(host(eta_r), host(eta_s))
+  same = (np.testing.assert_array_equal if lane_elements == 1
+          else (lambda a, b, err_msg="": close(a, b, what=err_msg)))
+  same(host(uN), host(snaps[nsteps]), err_msg="u^N")
+  same(host(w_r), host(w_s), err_msg="w^0")
+  same(host(eta_r), host(eta_s), err_msg="eta")
 
 
 def test_record_in_place_and_flags(pkg, gpu):
@@ -226,9 +264,9 @@ def rec_sweep(op, u0, dt, nsteps, t0=0.0):
 ])
 def test_pair_tiles_equal_one_element_per_lane(pkg, gpu, N, K, batch, rtw, spl, nsteps, inflow,
                                                refined):
-  """The record sweeps on pair tiles (two consecutive elements per lane, dg_rec.hip) against
-  the one-element-per-lane record kernels at the same steps per launch: record, final state,
-  w^0 and |eta| bit for bit (tile shape never changes the arithmetic)."""
+  """The record sweeps on pair tiles (two consecutive elements per lane, Horner-form steps,
+  dg_rec.hip) against the one-element-per-lane stage-loop record kernels at the same steps
+  per launch: record, final state, w^0 and |eta| to HORNER_RTOL (resolved jumps)."""
   v_x = np.linspace(0.0, 1.0, K + 1)
   if refined:
     for k in (2, K // 3, K // 3 + 1, K - 1):
@@ -237,18 +275,17 @@ def test_pair_tiles_equal_one_element_per_lane(pkg, gpu, N, K, batch, rtw, spl, 
   op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
   assert op.uniform != refined
   dt = mesh.cfl_dt()
-  u0 = op.new_field()
-  rng = np.random.default_rng(N * 1000 + K)
-  op.init_sine(rng.uniform(0.5, 1.5, batch), rng.integers(1, 5, batch).astype(float),
-               rng.uniform(0, 6, batch), out=u0)
+  u0 = noisy_sine(op, N * 1000 + K, batch)
   op.tune(rec_tile_width=2, rec_steps_per_launch=spl, rec_lane_elements=1)
   assert (op.rec_steps_per_launch, op.rec_lane_elements) == (spl, 1)
   ref = rec_sweep(op, u0, dt, nsteps, t0=0.02)
   op.tune(rec_tile_width=rtw, rec_steps_per_launch=spl, rec_lane_elements=2)
   assert (op.rec_tile_width, op.rec_steps_per_launch, op.rec_lane_elements) == (rtw, spl, 2)
   got = rec_sweep(op, u0, dt, nsteps, t0=0.02)
-  for name, a, b in zip(("record", "u^N", "w^0", "|eta|"), got, ref):
-    np.testing.assert_array_equal(a, b, err_msg=name)
+  umax = float(np.abs(host(u0)).max())
+  np.testing.assert_allclose(got[0], ref[0], rtol=0, atol=HORNER_RTOL * umax, err_msg="record")
+  for name, a, b in zip(("u^N", "w^0", "|eta|"), got[1:], ref[1:]):
+    close(a, b, what=name)
   assert np.abs(ref[3]).max() > 0
 
 
