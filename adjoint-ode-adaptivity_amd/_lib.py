@@ -23,9 +23,11 @@ DG_TUNE_REC_TILE_WIDTH, DG_TUNE_REC_STEPS_PER_LAUNCH = 5, 6
 DG_TUNE_REC_LANE_ELEMENTS, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 7, 8
 DG_TUNE_P_TILE_WIDTH, DG_TUNE_P_STEPS_PER_LAUNCH = 9, 10
 DG_TUNE_REC_FWD_TILE_WIDTH = 11
+DG_TUNE_REC_SWEEP = 12
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
+DG_SWEEP_TERMINAL_STATE = 4
 
 _c_dbl_p = ctypes.POINTER(ctypes.c_double)
 _vp = ctypes.c_void_p
@@ -59,6 +61,11 @@ SIGNATURES = {
                                  _vp]),
     "dg_lserk4_adj_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,
                                  _i32, _vp]),
+    "dg_lserk4_sweep_rec": (_i32, [_vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
+                                   _i32, _vp, _i32, _vp]),
+    "dg_plan_query_sweep": (_i32, [_vp, _i32, _vp]),
+    "dg_sweep_status": (_i32, [_vp, ctypes.POINTER(_i32), _vp]),
+    "dg_plan_sweep_trace": (_i32, [_vp, _vp]),
     "dg_plan_query_p": (_i32, [_vp, _vp]),
     "dg_prolong": (_i32, [_vp, _vp, _c_dbl_p, _vp, _vp, _vp]),
     "dg_lserk4_adj_p": (_i32, [_vp, _vp, _c_dbl_p, _vp, _vp, ctypes.c_double, ctypes.c_double,

@@ -11,8 +11,10 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(_HERE, "csrc", f) for f in ("dg_advec.hip", "dg_burgers.hip", "dg_wave.hip", "dg_time.hip", "dg_fd.hip",
-                                                     "dg_util.hip", "dg_rec.hip", "dg_dwr.hip")]
+                                                     "dg_util.hip", "dg_rec.hip", "dg_dwr.hip",
+                                                     "dg_sweep.hip")]
 COMMON = os.path.join(_HERE, "csrc", "dg_common.h")
+HEADERS = [COMMON, os.path.join(_HERE, "csrc", "dg_rec_tiles.h")]
 INCLUDE = os.path.normpath(os.path.join(_HERE, "..", "include"))
 OUT = os.path.join(_HERE, "lib", "libdgadv.so")
 ARCH = os.environ.get("DG_OFFLOAD_ARCH", "gfx950")
@@ -29,7 +31,7 @@ def build(force=False, verbose=True, extra_flags=(), out=None):
   """Build lib/libdgadv.so; `out` + `extra_flags` build an experiment variant elsewhere
   (its own object directory; the product library is untouched)."""
   OUT_ = OUT if out is None else os.path.abspath(out)
-  deps = SRCS + [COMMON, os.path.join(INCLUDE, "dg_advec.h")]
+  deps = SRCS + HEADERS + [os.path.join(INCLUDE, "dg_advec.h")]
   if (not force and os.path.exists(OUT_)
       and os.path.getmtime(OUT_) >= max(os.path.getmtime(d) for d in deps)):
     if verbose:

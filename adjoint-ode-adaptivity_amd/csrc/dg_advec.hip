@@ -1067,6 +1067,50 @@ inline int chunk(const dg_plan* p, int left) {
   while (m > left) m >>= 1;
   return m < 1 ? 1 : m;
 }
+
+// The dataflow sweep's blocks for `nsteps` steps (dg_sweep.hip): true with the forward /
+// adjoint steps per block when the plan runs it -- pair tiles of 1024 elements in both
+// directions, the record shape's 10- or 20-step forward and 10-step adjoint launches as its
+// blocks, nsteps a multiple of both and at most sweep_max_steps() -- else false (the
+// launch-per-block pair runs, with the same results).
+bool sweep_shape(const dg_plan* p, int nsteps, int* msf, int* msa) {
+  const int f = rec_msteps_fwd(p), a = rec_msteps(p);
+  *msf = f;
+  *msa = a;
+  return p->rec_sweep && rec_pairs(p) && rec_fwd_width(p) == 2 && p->rec_tile_width == 2 &&
+         (f == 10 || f == 20) && a == 10 && nsteps > 0 && nsteps % f == 0 && nsteps % a == 0 &&
+         nsteps <= sweep_max_steps();
+}
+
+// The plan's dataflow scratch: a control region of sync words and flags (zeroed once, then
+// kept consistent by the kernel's epochs) followed by a data region (block states, indicator
+// partials).  Grows the control region to `sync_bytes` (zeroing what it newly covers, which
+// an earlier call may have used as data) and the allocation to hold `data_bytes` after it.
+// *data = the data region's start.
+int sweep_scratch(dg_plan* p, size_t sync_bytes, size_t data_bytes, hipStream_t st, char** data) {
+  const size_t sync = sync_bytes > p->sweep_sync ? sync_bytes : p->sweep_sync;
+  if (!p->d_sweep || p->sweep_bytes < sync + data_bytes) {
+    if (p->d_sweep) {
+      HIP_TRY(hipStreamSynchronize(st));  // an earlier sweep may still use it
+      (void)hipFree(p->d_sweep);
+      p->d_sweep = nullptr;
+      p->sweep_bytes = p->sweep_sync = 0;
+      p->sweep_items = -1;
+    }
+    if (hipMalloc(&p->d_sweep, sync + data_bytes) != hipSuccess) {
+      p->d_sweep = nullptr;
+      return fail(DG_ERR_NOMEM, "hipMalloc of the dataflow sweep's scratch failed");
+    }
+    p->sweep_bytes = sync + data_bytes;
+  }
+  if (sync > p->sweep_sync) {
+    HIP_TRY(hipMemsetAsync(static_cast<char*>(p->d_sweep) + p->sweep_sync, 0,
+                           sync - p->sweep_sync, st));
+    p->sweep_sync = sync;
+  }
+  *data = static_cast<char*>(p->d_sweep) + sync;
+  return DG_OK;
+}
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1203,6 +1247,17 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
       if (k == 1 || k == 2 || k == 4 || k == 8) p->p_msteps = k;
     }
   }
+  if (const char* v = std::getenv("DG_REC_SWEEP")) {
+    const int k = std::atoi(v);
+    if (k == 0 || k == 1) p->rec_sweep = k;
+  }
+  {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      p->cu_count = cus;
+    if (p->cu_count < 1) p->cu_count = 1;
+  }
   auto cleanup = [&](const std::string& m) {
     dg_plan_destroy(p);
     return fail(DG_ERR_NOMEM, m);
@@ -1232,6 +1287,7 @@ int dg_plan_destroy(dg_plan* p) {
   if (p->d_scratch2) (void)hipFree(p->d_scratch2);
   if (p->d_pv) (void)hipFree(p->d_pv);
   if (p->d_pi) (void)hipFree(p->d_pi);
+  if (p->d_sweep) (void)hipFree(p->d_sweep);
   delete p;
   return DG_OK;
 }
@@ -1311,6 +1367,10 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       if (value != 1 && value != 2)
         return fail(DG_ERR_ARG, "record lane elements must be 1 or 2");
       p->rec_lane_elems = int(value);
+      return DG_OK;
+    case DG_TUNE_REC_SWEEP:
+      if (value != 0 && value != 1) return fail(DG_ERR_ARG, "record sweep mode must be 0 or 1");
+      p->rec_sweep = int(value);
       return DG_OK;
     case DG_TUNE_TILE_WIDTH:
       if (value != 1 && value != 2) return fail(DG_ERR_ARG, "tile width must be 1 or 2");
@@ -1623,6 +1683,114 @@ int dg_lserk4_adj_rec(dg_plan* p, double* w, const double* jumps, double t0, dou
   }
   if (in != w)
     HIP_TRY(hipMemcpyAsync(w, in, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
+  return DG_OK;
+}
+
+int dg_lserk4_sweep_rec(dg_plan* p, const double* u0, double* uN, double* w, double* jumps,
+                        double t0, double dt, int nsteps, double* eta, int flags, void* stream) {
+  if (!p || !u0 || !w || (!jumps && nsteps > 0)) return fail(DG_ERR_ARG, "null argument");
+  if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
+  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS | DG_SWEEP_TERMINAL_STATE))
+    return fail(DG_ERR_ARG, "unknown flags");
+  if (p->nonlinear() || p->nstages != 5)
+    return fail(DG_ERR_ARG, "the jump record is the linear LSERK4 sweep's (use snapshots)");
+  if (reinterpret_cast<uintptr_t>(jumps) % 16 != 0)
+    return fail(DG_ERR_ARG, "the jump record must be 16-byte aligned");
+  if (uN && (uN == w || uN == u0)) return fail(DG_ERR_ARG, "uN must not alias u0 or w");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool term = (flags & DG_SWEEP_TERMINAL_STATE) != 0;
+  const int aflags = flags & (DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS);
+  const int64_t field = p->ktot * p->NP;
+  const size_t fbytes = sizeof(double) * size_t(field);
+  int msf = 0, msa = 0;
+  if (!sweep_shape(p, nsteps, &msf, &msa)) {
+    // the launch-per-block pair: forward into uN (or w when it is the terminal weight, or a
+    // scratch field), then the adjoint in place on w
+    double* fin = uN;
+    if (!fin && term) fin = w;
+    if (!fin) {
+      char* data = nullptr;
+      if (const int rc = sweep_scratch(p, 256, fbytes, st, &data)) return rc;
+      fin = reinterpret_cast<double*>(data);
+    }
+    if (const int rc = dg_lserk4_fwd_rec(p, u0, fin, t0, dt, nsteps, jumps, stream)) return rc;
+    if (term && fin != w) HIP_TRY(hipMemcpyAsync(w, fin, fbytes, hipMemcpyDeviceToDevice, st));
+    return dg_lserk4_adj_rec(p, w, jumps, t0, dt, nsteps, eta, aflags, stream);
+  }
+  const int nbF = nsteps / msf, nbA = nsteps / msa;
+  const int64_t items = sweep_items(p, msf, msa, nsteps);
+  const size_t sync_bytes = (sizeof(uint32_t) * size_t(sweep_sync_words() + items) + 255) & ~size_t(255);
+  // fields: forward block outputs U[1..nbF-1] (+ U[nbF] unless the caller keeps u^N), adjoint
+  // block outputs W[1..nbA-1] (+ a copy of the caller's terminal weight when one block would
+  // read and write w); partial indicator rows for nbA - 1 blocks
+  const int wcopy = (!term && nbA == 1) ? 1 : 0;
+  const int nfields = (nbF - 1) + (uN ? 0 : 1) + (nbA - 1) + wcopy;
+  const int nparts = eta ? nbA - 1 : 0;
+  const size_t bytes = sync_bytes + fbytes * size_t(nfields) + sizeof(double) * size_t(p->ktot) * size_t(nparts);
+  char* data = nullptr;
+  if (const int rc = sweep_scratch(p, sync_bytes, bytes - sync_bytes, st, &data)) return rc;
+  if (p->sweep_items != items) {
+    // the take counter numbers launches by items per launch: a new shape starts it afresh
+    HIP_TRY(hipMemsetAsync(p->d_sweep, 0, sync_bytes, st));
+    p->sweep_items = items;
+  }
+  double* fld = reinterpret_cast<double*>(data);
+  int next = 0;
+  SweepBufs b{};
+  b.sync = static_cast<uint32_t*>(p->d_sweep);
+  b.U[0] = const_cast<double*>(u0);
+  for (int k = 1; k < nbF; ++k) b.U[k] = fld + field * next++;
+  b.U[nbF] = uN ? uN : fld + field * next++;
+  if (term) {
+    b.W[0] = b.U[nbF];
+  } else if (wcopy) {
+    b.W[0] = fld + field * next++;
+    HIP_TRY(hipMemcpyAsync(b.W[0], w, fbytes, hipMemcpyDeviceToDevice, st));
+  } else {
+    b.W[0] = w;  // read by the first block, rewritten by the last (nbA >= 2: no tile overlap)
+  }
+  for (int k = 1; k < nbA; ++k) b.W[k] = fld + field * next++;
+  b.W[nbA] = w;
+  b.rec = jumps;
+  b.eta = eta;
+  b.part = nparts ? fld + field * next : nullptr;
+  const int mode = eta ? (kEtaOn | ((aflags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
+                          ((aflags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
+                       : 0;
+  return sweep_launch_rec(p, msf, b, t0, dt, nsteps, mode, st);
+}
+
+int dg_plan_query_sweep(const dg_plan* p, int nsteps, int64_t out[4]) {
+  if (!p || !out) return fail(DG_ERR_ARG, "null argument");
+  int msf = 0, msa = 0;
+  const bool on = sweep_shape(p, nsteps, &msf, &msa);
+  out[0] = on ? 1 : 0;
+  out[1] = msf;
+  out[2] = msa;
+  out[3] = on ? sweep_items(p, msf, msa, nsteps) : 0;
+  return DG_OK;
+}
+
+int dg_plan_sweep_trace(dg_plan* p, uint64_t* trace) {
+  if (!p) return fail(DG_ERR_ARG, "null plan");
+  p->sweep_trace = trace;
+  return DG_OK;
+}
+
+int dg_sweep_status(dg_plan* p, int* status, void* stream) {
+  if (!p || !status) return fail(DG_ERR_ARG, "null argument");
+  *status = 0;
+  if (!p->d_sweep) return DG_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  uint32_t* err = static_cast<uint32_t*>(p->d_sweep) + sweep_err_word();
+  uint32_t h = 0;
+  HIP_TRY(hipMemcpyAsync(&h, err, sizeof(h), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (h) {
+    HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  *status = int(h);
   return DG_OK;
 }
 

@@ -446,6 +446,16 @@ struct dg_plan {
   // 512 elements), steps per launch 1, 2, 4 or 8 (8 on 512-element tiles)
   int p_tile_width = 2;
   int p_msteps = 4;
+  // the dataflow sweep (dg_lserk4_sweep_rec, dg_sweep.hip): its scratch (sync words, block
+  // states, indicator partials; grown on demand) and the switch (1: one dataflow launch where
+  // the shape allows it, 0: the launch-per-block pair)
+  void* d_sweep = nullptr;
+  size_t sweep_bytes = 0;
+  size_t sweep_sync = 0;  // bytes of its control region (zeroed, then kept by epochs)
+  int64_t sweep_items = -1;  // work items of the last dataflow launch on that region
+  int rec_sweep = 1;
+  uint64_t* sweep_trace = nullptr;  // dg_plan_sweep_trace: per-item timestamps (profiling)
+  int cu_count = 0;  // compute units of the plan's device (the dataflow grid)
   int xcd_order = 1;  // XCD-aware tile order
   int lane_elems = 0;  // 0: workgroup tiles (one element per lane); 2 or 4: wave tiles
   // physics (dg_plan_set_physics): DG_FLUX_LINEAR / DG_FLUX_BURGERS, SlopeLimitN per stage
@@ -574,6 +584,25 @@ int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
 // plan->lane_elems; `times` as for the workgroup-tile launchers.
 int wave_launch_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
                      const double* times, double dt, hipStream_t st);
+
+// The dataflow sweep (dg_sweep.hip): buffers of one launch.  U[b]: forward block b's input
+// (U[0] = u0, U[nbF] = u^N), W[a]: adjoint block a's input (W[0] the terminal weight,
+// W[nbA] the caller's w); part: (nbA - 1) rows of ktot indicator partials; sync: the
+// sweep_sync_words() control words followed by one flag per item.
+struct SweepBufs {
+  double* U[5];
+  double* W[5];
+  double* rec;
+  double* eta;
+  double* part;
+  uint32_t* sync;
+};
+int64_t sweep_items(const dg_plan* p, int msf, int msa, int nsteps);
+int sweep_launch_rec(dg_plan* p, int msf, const SweepBufs& b, double t0, double dt, int nsteps,
+                     int mode, hipStream_t st);
+int sweep_sync_words();
+int sweep_max_steps();
+int sweep_err_word();
 
 // Jump-record sweep launches on pair tiles (dg_rec.hip), selected by plan->rec_lane_elems == 2.
 int pair_launch_step_rec(const dg_plan* p, int ms, const double* in, double* rec, double* last,

@@ -1,0 +1,281 @@
+// dg_sweep.hip — the jump-record sweep pair as ONE dataflow launch (dg_lserk4_sweep_rec).
+//
+// The launch-per-block sweep (dg_lserk4_fwd_rec + dg_lserk4_adj_rec, dg_rec.hip) runs three
+// launches per 20-step sweep at the default shape (forward 20, adjoint 10 + 10), and each
+// launch pays a fill (the first round of workgroups loading their tiles with nothing to
+// overlap) and a drain (the last round running partly empty: at K = 2^20 the forward's 1,279
+// tiles are 1.66 rounds of the 768 resident workgroups).  Here the same tile bodies
+// (dg_rec_tiles.h, policy WT = write-through hand-offs) are the work items of ONE launch:
+//   items, in queue order: forward block 0 tiles 0..nTF-1, forward block 1 tiles, ...,
+//   adjoint block 0 tiles 0..nTA-1 (reverse steps nsteps-MSA..nsteps-1), adjoint block 1, ...
+//   The grid has one workgroup per item; each takes the next item from one counter when the
+//   hardware starts it (not by blockIdx), so items start in queue order.  An item waits only
+//   for items earlier in the queue -- the previous block's tiles whose output ranges its
+//   input range (tile + halo) touches; the first adjoint block for the last forward block's
+//   tiles covering its range (whose completion implies every earlier forward block's records
+//   there) -- so the sweep cannot deadlock at any residency: the earliest waiting item's
+//   producers were taken before it by workgroups that are running and wait on nothing later.
+//   (A persistent grid looping over items measured 143 VGPRs: the compiler keeps both
+//   bodies' constants live across the loop; one item per workgroup keeps the registers of
+//   the separate kernels.)
+// Hand-offs (cdna_hip_programming.md §6 Guideline 16, R1; MI355X_MICROARCH.md, visibility):
+//   producer: every store of handed-off bytes (block states, the record, indicator partials)
+//     is write-through (`sc1`); every wave drains (`s_waitcnt vmcnt(0)`), a workgroup barrier,
+//     then one lane stores the item's flag (an agent-scope atomic store of the epoch);
+//   consumer: wave 0 polls the producers' flags (relaxed agent loads, one lane per flag,
+//     `s_sleep` between polls), a workgroup barrier, then EVERY load of handed-off bytes is
+//     an `sc1` load (bypasses the CU's L1), so no acquire fence is needed;
+//   no buffer is written twice in a launch (every block writes its own state buffer; the
+//   adjoint's indicator partials have one row per block), so no cache line another
+//   workgroup reads can change after it was read.
+// Epochs: a 64-bit take counter that only grows numbers the launches (value / items) and the
+// items (value % items); the flags hold the launch's epoch, so no memset precedes a launch
+// of the same shape and HIP-graph replays work.  Every poll is bounded: a producer that never finishes (a bug) sets
+// the error word after ~2^20 polls and every waiter gives up, so the launch always ends;
+// dg_sweep_status() reports it.
+// The results are bit-identical to the launch-per-block pair with the same steps per block
+// (same tile arithmetic; the indicator's block partials are added in launch order).
+#include "dg_rec_tiles.h"
+
+namespace {
+using namespace dgk;
+using namespace dgr;
+
+constexpr int kSweepMaxSteps = 40;   // steps per sweep (the forward blocks' constants are kernargs)
+constexpr int kSweepMaxBlocks = 4;   // blocks per direction (kSweepMaxSteps / 10)
+// control words (uint32 index): a 64-bit take counter, the error word, then one flag per item
+constexpr int kSyncHead = 0, kSyncErr = 2, kSyncFlags = 16;
+constexpr int kSweepSpinLimit = 1 << 20;
+#ifndef DG_SWEEP_WAVES
+#define DG_SWEEP_WAVES 5
+#endif
+
+template <int NP, int MSF> struct SweepArgs {
+  RpOp<NP> c;
+  double bnd[(kSweepMaxSteps / MSF) * (MSF * 6 + 1)];  // block b's rp_block_bnd at b*(6 MSF+1)
+  double* U[kSweepMaxBlocks + 1];  // forward block b reads U[b] (U[0] = u0), writes U[b+1]
+  double* W[kSweepMaxBlocks + 1];  // adjoint block a reads W[a] (terminal weight), writes W[a+1]
+  double* rec;
+  double* eta;
+  double* part;                    // (nbA - 1) rows of ktot: the adjoint blocks' partial eta
+  const double* scale;
+  uint32_t* sync;                  // kSync* words, then one flag per item
+  uint64_t* trace;                 // nullable: per item {dequeued, producers done, published,
+                                   // XCC id << 32 | workgroup id} (wall clock, 100 MHz)
+  int32_t nbF, nbA, nTF, nTA;
+  int32_t nsteps;
+  int32_t mode;                    // kEta* bits (0: no indicator)
+  int32_t spin_limit;
+};
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0: wait until flags[0..nd) all hold `epoch` (one lane per flag, nd <= 64).
+__device__ __forceinline__ void sweep_wait(const uint32_t* flags, int nd, uint32_t epoch,
+                                           uint32_t* sync, int limit) {
+  const int l = threadIdx.x & 63;
+  bool ok = l >= nd;
+  if (!ok) ok = ld_agent(flags + l) == epoch;
+  int spins = 0;
+  while (!__all(ok)) {
+    __builtin_amdgcn_s_sleep(2);
+    if (!ok) ok = ld_agent(flags + l) == epoch;
+    if (++spins >= limit) {  // a producer that never finishes: flag the sweep, give up
+      if (l == 0) st_agent(sync + kSyncErr, 1u);
+      break;
+    }
+    if ((spins & 255) == 0 && ld_agent(sync + kSyncErr) != 0u) break;  // someone gave up
+  }
+}
+
+template <int NP, bool UNI, int MSF, int MSA>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WAVES))) void k_sweep_rp(
+    SweepArgs<NP, MSF> a) {
+  constexpr int NW = 8, E = 2;
+  using G = RpGeo<NP, NW, E>;
+  constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
+  constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MSF * 6 + 1];
+  __shared__ uint32_t s_item, s_epoch;
+  uint32_t* sync = a.sync;
+  uint32_t* flags = sync + kSyncFlags;
+  const int tid = threadIdx.x;
+  const int64_t ktot = a.c.ktot;
+  const int nTF = a.nTF, nTA = a.nTA, nbF = a.nbF, nbA = a.nbA;
+  const int64_t nF = int64_t(nbF) * nTF;
+  const int64_t nItems = nF + int64_t(nbA) * nTA;
+  if (tid == 0) {
+    // The take counter only grows: every launch of this shape takes exactly nItems values
+    // (one per workgroup), so h / nItems numbers the launch (its epoch - 1) and h % nItems is
+    // the item -- no reset, no generation word, no exit counter.  (The host zeroes the
+    // control words when a launch of another shape reuses them.)
+    const uint64_t h = __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(sync + kSyncHead),
+                                              uint64_t(1), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    s_epoch = uint32_t(h / uint64_t(nItems)) + 1u;
+    s_item = uint32_t(h % uint64_t(nItems));
+  }
+  __syncthreads();
+  const int64_t item = s_item;
+  const uint32_t epoch = s_epoch;
+  const uint64_t t_deq = a.trace ? uint64_t(wall_clock64()) : 0;
+  {
+    // decode the item and the range of flags it waits for
+    const bool fwd = item < nF;
+    int blk, j;
+    int64_t d0 = 0;
+    int nd = 0;
+    if (fwd) {
+      blk = int(item / nTF);
+      j = int(item - int64_t(blk) * nTF);
+      if (blk > 0) {  // the previous block's tiles j-1..j+1 (halo < TEF)
+        const int lo = j > 0 ? j - 1 : 0, hi = j + 1 < nTF ? j + 1 : nTF - 1;
+        d0 = int64_t(blk - 1) * nTF + lo;
+        nd = hi - lo + 1;
+      }
+    } else {
+      const int64_t i2 = item - nF;
+      blk = int(i2 / nTA);
+      j = int(i2 - int64_t(blk) * nTA);
+      if (blk == 0) {  // the last forward block's tiles covering the input + record range
+        int64_t elo = int64_t(j) * TEA - HA, ehi = int64_t(j + 1) * TEA + HA;
+        elo = elo > 0 ? elo : 0;
+        ehi = ehi < ktot - 1 ? ehi : ktot - 1;
+        const int lo = int(elo / TEF), hi = int(ehi / TEF);
+        d0 = int64_t(nbF - 1) * nTF + lo;
+        nd = hi - lo + 1;
+      } else {
+        const int lo = j > 0 ? j - 1 : 0, hi = j + 1 < nTA ? j + 1 : nTA - 1;
+        d0 = nF + int64_t(blk - 1) * nTA + lo;
+        nd = hi - lo + 1;
+      }
+    }
+    if (tid < 64 && nd > 0) sweep_wait(flags + d0, nd, epoch, sync, a.spin_limit);
+    // no acquire fence: every load of handed-off bytes below is an sc1 load; this only keeps
+    // the compiler from hoisting them above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    const uint64_t t_ready = a.trace ? uint64_t(wall_clock64()) : 0;
+    if (fwd) {
+      const int64_t e0 = int64_t(j) * TEF - HF;
+      using SA = SweepArgs<NP, MSF>;
+      const double* kb = reinterpret_cast<const double*>(
+                             kernarg_tail<decltype(&k_sweep_rp<NP, UNI, MSF, MSA>), SA>() +
+                             offsetof(SA, bnd)) + blk * (MSF * 6 + 1);
+      const int64_t n0 = int64_t(blk) * MSF;
+      const bool jend = blk == a.nbF - 1;
+      if (edge_tile(e0, G::T, ktot, a.c.K))
+        rp_step_tile<NP, UNI, NW, E, MSF, true, true>(lds, j, a.U[blk], a.rec, a.U[blk + 1],
+                                                      a.scale, a.c, kb, n0, jend);
+      else
+        rp_step_tile<NP, UNI, NW, E, MSF, false, true>(lds, j, a.U[blk], a.rec, a.U[blk + 1],
+                                                       a.scale, a.c, kb, n0, jend);
+    } else {
+      const int64_t e0 = int64_t(j) * TEA - HA;
+      const bool lastb = blk == a.nbA - 1;
+      EtaSink es;
+      es.eta = a.eta;
+      es.part_out = (a.mode && !lastb) ? a.part + int64_t(blk) * ktot : nullptr;
+      es.part_in = a.part;
+      es.part_ld = ktot;
+      es.nparts = lastb ? a.nbA - 1 : 0;
+      es.mode = a.mode;
+      const int64_t n0 = int64_t(a.nsteps) - int64_t(blk + 1) * MSA;
+      if (edge_tile(e0, G::T, ktot, a.c.K))
+        rp_adj_tile<NP, UNI, NW, E, MSA, true, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
+                                                     a.scale, a.c, n0);
+      else
+        rp_adj_tile<NP, UNI, NW, E, MSA, false, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
+                                                      a.scale, a.c, n0);
+    }
+    // publish: every wave's write-through stores have completed, then one flag store
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_agent(flags + item, epoch);
+    if (a.trace && tid == 0) {
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint64_t* tr = a.trace + 4 * item;
+      tr[0] = t_deq;
+      tr[1] = t_ready;
+      tr[2] = uint64_t(wall_clock64());
+      tr[3] = (uint64_t(xcc) << 32) | blockIdx.x;
+    }
+  }
+}
+
+static_assert(kSweepMaxBlocks + 1 == sizeof(SweepBufs::U) / sizeof(double*), "SweepBufs");
+
+template <int NP, bool UNI, int MSF, int MSA>
+int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int nsteps,
+                 int mode, hipStream_t st) {
+  SweepArgs<NP, MSF> a;
+  if (const int rc = rp_make_op<NP>(p, dt, &a.c)) return rc;
+  const int nbF = nsteps / MSF, nbA = nsteps / MSA;
+  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt (One_code.mlx:139)
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  for (int bk = 0; bk < nbF; ++bk)
+    rp_block_bnd(p, MSF, &tn[size_t(bk) * MSF], dt, a.bnd + bk * (MSF * 6 + 1));
+  for (int i = 0; i <= kSweepMaxBlocks; ++i) {
+    a.U[i] = b.U[i];
+    a.W[i] = b.W[i];
+  }
+  a.rec = b.rec;
+  a.eta = b.eta;
+  a.part = b.part;
+  a.scale = p->d_scale;
+  a.sync = b.sync;
+  a.trace = p->sweep_trace;
+  a.nbF = nbF;
+  a.nbA = nbA;
+  using G = RpGeo<NP, 8, 2>;
+  a.nTF = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSF>::F));
+  a.nTA = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSA>::A));
+  a.nsteps = nsteps;
+  a.mode = mode;
+  a.spin_limit = kSweepSpinLimit;
+  const int64_t items = int64_t(nbF) * a.nTF + int64_t(nbA) * a.nTA;
+  hipLaunchKernelGGL((k_sweep_rp<NP, UNI, MSF, MSA>), dim3(unsigned(items)), dim3(512), 0, st, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+template <int NP>
+int sweep_np(dg_plan* p, int msf, const dgk::SweepBufs& b, double t0, double dt, int nsteps,
+             int mode, hipStream_t st) {
+  if (msf == 20)
+    return p->uniform ? sweep_launch<NP, true, 20, 10>(p, b, t0, dt, nsteps, mode, st)
+                      : sweep_launch<NP, false, 20, 10>(p, b, t0, dt, nsteps, mode, st);
+  return p->uniform ? sweep_launch<NP, true, 10, 10>(p, b, t0, dt, nsteps, mode, st)
+                    : sweep_launch<NP, false, 10, 10>(p, b, t0, dt, nsteps, mode, st);
+}
+
+}  // namespace
+
+namespace dgk {
+
+int64_t sweep_items(const dg_plan* p, int msf, int msa, int nsteps) {
+  constexpr int T = 1024;
+  const int64_t nTF = grid_for(p->ktot, T - 2 * ((msf * 5 + 2) & ~1));
+  const int64_t nTA = grid_for(p->ktot, T - 2 * ((msa * 5 + 1) & ~1));
+  return int64_t(nsteps / msf) * nTF + int64_t(nsteps / msa) * nTA;
+}
+
+int sweep_launch_rec(dg_plan* p, int msf, const SweepBufs& b, double t0, double dt,
+                     int nsteps, int mode, hipStream_t st) {
+  int rc = DG_OK;
+  DG_DISPATCH_NP(p->NP, rc = sweep_np<NP>(p, msf, b, t0, dt, nsteps, mode, st));
+  return rc;
+}
+
+int sweep_sync_words() { return kSyncFlags; }
+int sweep_max_steps() { return kSweepMaxSteps; }
+int sweep_err_word() { return kSyncErr; }
+
+}  // namespace dgk

@@ -138,19 +138,42 @@ class EnsembleSweep:
       self.op.adjoint(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta,
                       eta_assign=True, eta_abs=True)
 
+  @property
+  def dataflow(self):
+    """True when ``sweep`` runs forward + adjoint as ONE dataflow launch
+    (dg_lserk4_sweep_rec, jump record, the plan's shape allowing it)."""
+    return self.record == "jumps" and self.op.query_sweep(self.nsteps)[0]
+
+  def sweep(self):
+    """Forward + adjoint + |eta|.  Jump record: one dg_lserk4_sweep_rec call -- a single
+    dataflow launch where the record shape allows (csrc/dg_sweep.hip), else the two launch
+    chains; bit-identical either way (J = |u^N|^2/2: the terminal weight is u^N, w ends as
+    w^0).  Snapshots: ``forward`` then ``adjoint``."""
+    if self.record == "jumps":
+      self.op.sweep_rec(self.u0, self.jumps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
+                        eta_assign=True, eta_abs=True, terminal_state=True)
+    else:
+      self.forward()
+      self.adjoint()
+
   def capture(self):
-    """Capture the forward and adjoint sweeps as two HIP graphs (replayed by
-    forward_graph / adjoint_graph): the per-launch host work (operator constants, inflow
-    values) is baked in once and the kernels run back to back."""
+    """Capture the sweep as HIP graphs (replayed by sweep_graph, or forward_graph /
+    adjoint_graph for the two halves of the snapshot pair): the per-launch host work
+    (operator constants, inflow values) is baked in once and the kernels run back to back."""
     dev = self.op.device
     torch.cuda.synchronize(dev)
     side = torch.cuda.Stream(dev)
     side.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(side):  # warm-up outside capture
-      self.forward()
-      self.adjoint()
+    with torch.cuda.stream(side):  # warm-up outside capture (allocates the sweep scratch)
+      self.sweep()
     torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize(dev)
+    if self.dataflow:
+      g = torch.cuda.CUDAGraph()
+      with torch.cuda.graph(g):
+        self.sweep()
+      self._graphs = (g,)
+      return self
     gf, ga = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
     with torch.cuda.graph(gf):
       self.forward()
@@ -158,6 +181,13 @@ class EnsembleSweep:
       self.adjoint()
     self._graphs = (gf, ga)
     return self
+
+  def sweep_graph(self):
+    if len(self._graphs) == 1:
+      self._graphs[0].replay()
+    else:
+      self._graphs[0].replay()
+      self._graphs[1].replay()
 
   def forward_graph(self):
     self._graphs[0].replay()
@@ -172,8 +202,7 @@ class EnsembleSweep:
     return self.partial
 
   def run(self):
-    self.forward()
-    self.adjoint()
+    self.sweep()
     return self.reduce()
 
   def per_ic(self):

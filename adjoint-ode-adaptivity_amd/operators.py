@@ -136,7 +136,7 @@ class DGAdvection1D:
 
   def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None,
            rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
-           rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None):
+           rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None, rec_sweep=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -149,8 +149,11 @@ class DGAdvection1D:
     ``rec_fwd_steps_per_launch`` gives the forward its own steps per launch (setting
     ``rec_steps_per_launch`` applies to both directions and clears it);
     ``rec_fwd_tile_width`` likewise gives the forward its own tile width (0: the adjoint's;
-    setting ``rec_tile_width`` applies to both)."""
+    setting ``rec_tile_width`` applies to both).  ``rec_sweep`` (1, default / 0): ``sweep_rec``
+    runs both directions as one dataflow launch where the shape allows, or as the two launch
+    chains (bit-identical)."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
+                     (_lib.DG_TUNE_REC_SWEEP, rec_sweep),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
                      (_lib.DG_TUNE_REC_LANE_ELEMENTS, rec_lane_elements),
                      (_lib.DG_TUNE_REC_FWD_STEPS_PER_LAUNCH, rec_fwd_steps_per_launch),
@@ -309,6 +312,52 @@ class DGAdvection1D:
                                      _stream(self.device))
     _lib.check(rc, "dg_lserk4_adj_rec")
     return w, eta
+
+  def sweep_rec(self, u0, jumps, w, t0, dt, nsteps, uN=None, eta=None, eta_assign=False,
+                eta_abs=False, terminal_state=True):
+    """``forward_rec`` + ``adjoint_rec`` in one call (dg_lserk4_sweep_rec): u0 -> u^nsteps
+    (into ``uN`` if given), then the adjoint into ``w`` (w^0 on exit) from the terminal weight
+    u^nsteps (``terminal_state``: J = |u^N|^2/2, w's content ignored) or from w itself.  Where
+    the record shape allows, both directions run as one dataflow launch (``query_sweep``);
+    the results are bit-identical to the two calls either way."""
+    eta_p = None if eta is None else self._field(eta, "eta", self.ktot)
+    un_p = None if uN is None else self._field(uN, "uN")
+    flags = ((_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) |
+             (_lib.DG_ADJ_ETA_ABS if eta_abs else 0) |
+             (_lib.DG_SWEEP_TERMINAL_STATE if terminal_state else 0))
+    rc = self._lib.dg_lserk4_sweep_rec(self._plan, self._field(u0, "u0"), un_p,
+                                       self._field(w, "w"), self._jumps(jumps, nsteps),
+                                       float(t0), float(dt), int(nsteps), eta_p, int(flags),
+                                       _stream(self.device))
+    _lib.check(rc, "dg_lserk4_sweep_rec")
+    return w, eta
+
+  def query_sweep(self, nsteps):
+    """(dataflow, forward steps per block, adjoint steps per block, work items) of
+    ``sweep_rec`` for an ``nsteps`` sweep; dataflow False: the two launch chains run."""
+    q = (ctypes.c_int64 * 4)()
+    _lib.check(self._lib.dg_plan_query_sweep(self._plan, int(nsteps), q), "dg_plan_query_sweep")
+    return bool(q[0]), int(q[1]), int(q[2]), int(q[3])
+
+  def sweep_trace(self, trace):
+    """Profiling: record per work item of every later dataflow sweep {taken, producers done,
+    published (wall clock, 100 MHz), XCC id << 32 | workgroup} into ``trace`` (CUDA int64,
+    4 * ``query_sweep(nsteps)[3]`` entries); None turns it off."""
+    ptr = None
+    if trace is not None:
+      if not trace.is_cuda or trace.dtype != torch.int64 or not trace.is_contiguous():
+        raise TypeError("trace must be a contiguous CUDA int64 tensor")
+      ptr = ctypes.c_void_p(trace.data_ptr())
+    _lib.check(self._lib.dg_plan_sweep_trace(self._plan, ptr), "dg_plan_sweep_trace")
+    self._trace = trace
+
+  def sweep_status(self):
+    """0, or 1 if a dataflow sweep since the last call gave up waiting for a producer (its
+    outputs are garbage); synchronises the device stream."""
+    st = ctypes.c_int(0)
+    _lib.check(self._lib.dg_sweep_status(self._plan, ctypes.byref(st), _stream(self.device)),
+               "dg_sweep_status")
+    return int(st.value)
 
   def slope_limit(self, u, out=None, ids=None):
     """SlopeLimitN(u) (utils/SlopeLimitN.m:1-33); ids (int32, batch*K) marks limited cells."""

@@ -483,7 +483,7 @@ def main_config3(args, world, rank, dev):
   if rank == 0 and world == 1 and not args.no_cpu_baseline:
     out["cpu_baseline"] = cpu_baseline_config3(N, K, 2)
   if rank == 0:
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out, allow_nan=False), flush=True)
   if world > 1:
     import torch.distributed as dist
     dist.destroy_process_group()
@@ -566,10 +566,23 @@ def main(argv=None):
     sweep.capture()  # each sweep becomes one HIP graph launch
   stream = torch.cuda.current_stream(dev)
   res_host = torch.zeros(2, dtype=torch.int64).pin_memory()  # refine index, value bits
+  # The jump record's sweep as ONE dataflow launch (dg_lserk4_sweep_rec, csrc/dg_sweep.hip)
+  # where the plan's shape allows: forward and adjoint are then not separately timeable.
+  dataflow = sweep.dataflow
 
   def one_step(ev=None):
     if ev:
       ev[0].record(stream)
+    if dataflow:
+      sweep.sweep_graph() if args.graph else sweep.sweep()
+      if ev:
+        ev[2].record(stream)
+      partial = sweep.reduce()
+      ens.gather_indicator(partial, n_total, reducer)
+      if args.gather_ics:
+        ens.gather_per_ic(sweep.per_ic(), n_total)
+      res_host.copy_(reducer.state[0:2], non_blocking=True)
+      return
     sweep.forward_graph() if args.graph else sweep.forward()
     if ev:
       ev[1].record(stream)
@@ -624,8 +637,12 @@ def main(argv=None):
     ms, tw = ((sweep.est.steps_per_launch, sweep.est.tile_width) if pmode
               else (fms, sweep.op.tile_width))
   chunks, fchunks = sweep_chunks(nsteps, ms), sweep_chunks(nsteps, fms)
-  fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / len(fchunks) for e in evs]
-  adj_us = [e[3].elapsed_time(e[2]) * 1e3 / len(chunks) for e in evs]
+  if dataflow:  # one launch per sweep: its time, reported in the adjoint's slot
+    fwd_us = [float("nan") for e in evs]
+    adj_us = [e[0].elapsed_time(e[2]) * 1e3 for e in evs]
+  else:
+    fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / len(fchunks) for e in evs]
+    adj_us = [e[3].elapsed_time(e[2]) * 1e3 / len(chunks) for e in evs]
   prolong_us = [e[1].elapsed_time(e[3]) * 1e3 for e in evs] if pmode else None
   step_ms = [evs[i][0].elapsed_time(evs[i + 1][0] if i + 1 < len(evs) else ev_end)
              for i in range(len(evs))]
@@ -641,7 +658,13 @@ def main(argv=None):
   # are the sweep's averages: achieved = sweep bytes / sweep time.
   #   p-estimate (k_adj_p): reads w^{n+m} and writes w^n at order N+1 (16 (Np + 1) B per
   #     element), reads the m + 1 order-N snapshots u^n..u^{n+m} (8 (m + 1) Np B), updates eta.
-  if args.record == "jumps":
+  #   dataflow: the one launch moves the sum of its blocks' bytes (the forward blocks' and the
+  #     adjoint blocks' figures above; a block's partial indicator row is written and read
+  #     once, as the launches' read-modify-write of eta).
+  if dataflow:
+    fwd_bytes = float(np.sum([(16.0 * Np + 8.0 * m) * ktot for m in fchunks]))
+    adj_bytes = fwd_bytes + float(np.sum([(16.0 * Np + 8.0 * m + 16.0) * ktot for m in chunks]))
+  elif args.record == "jumps":
     fwd_bytes = float(np.mean([(16.0 * Np + 8.0 * m) * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 * Np + 8.0 * m + 16.0) * ktot for m in chunks]))
   elif pmode:
@@ -656,6 +679,8 @@ def main(argv=None):
   kadj, kstep = ("k_adj_rp", "k_step_rp") if pairs else ("k_adj", "k_step")
   if pmode:
     kadj = "k_adj_p"
+  if dataflow:
+    kadj = "k_sweep_rp"
   tile_tag = tile_tag_fwd = f"{tw},2 elements/lane" if pairs else f"{tw}"
   # Issued vs useful lanes: each tile recomputes a halo of H elements per side (the
   # dependency cone of its fused steps) and writes T - 2H, weighted by steps.
@@ -687,7 +712,7 @@ def main(argv=None):
       with open(PROFILE_TRAFFIC[args.record]) as f:
         tr = json.load(f)
       if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
-          and tr.get("steps_per_launch") == ms
+          and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
           and tr.get("record", "snapshots") == args.record):
         traffic = tr.get("adj_bytes_per_launch")
         traffic_src = tr.get("source")
@@ -698,8 +723,11 @@ def main(argv=None):
   # the snapshot algorithm moves for the same steps) -- an effective rate, not HBM traffic.
   effective = None
   if args.record == "jumps":
-    snap_fwd = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
-    snap_adj = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
+    agg = np.sum if dataflow else np.mean
+    snap_fwd = float(agg([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
+    snap_adj = float(agg([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
+    if dataflow:
+      snap_adj += snap_fwd
     eff_adj = snap_adj / (adj_launch_us * 1e-6) / 1e9
     eff_fwd = snap_fwd / (fwd_launch_us * 1e-6) / 1e9
     effective = {"what": "launch times priced with the snapshot sweep's algorithmic bytes for "
@@ -722,6 +750,12 @@ def main(argv=None):
   fwd_fpu = eo_flops_per_update(Np, False)
   adj_tf = adj_fpu * upl / (adj_launch_us * 1e-6) / 1e12
   fwd_tf = fwd_fpu * fupl / (fwd_launch_us * 1e-6) / 1e12
+  if dataflow:
+    # the one launch executes both directions' flops; its issued lanes weight each
+    # direction's halo factor by its share of them
+    f_fl, a_fl = fwd_fpu * Np * ktot * nsteps, adj_fpu * Np * ktot * nsteps
+    adj_tf = (f_fl + a_fl) / (adj_launch_us * 1e-6) / 1e12
+    halo_adj = (f_fl * halo_fwd + a_fl * halo_adj) / (f_fl + a_fl)
   resolved = indicator_resolution(sweep, N, K)
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
@@ -807,6 +841,30 @@ def main(argv=None):
   }
   if pmode:
     out["prolong_us"] = float(np.mean(prolong_us))
+  if dataflow:
+    r = out["roofline"]
+    r["kernel"] = (f"k_sweep_rp<{Np},uniform,1024 elements,fwd {'+'.join(map(str, fchunks))},"
+                   f"adj {'+'.join(map(str, chunks))},jumps> (ONE dataflow launch per sweep: "
+                   f"{nsteps} forward + {nsteps} reverse steps + DWR)")
+    r["note"] = ("dataflow sweep (dg_lserk4_sweep_rec): the forward and adjoint blocks' tiles are "
+                 "the work items of one launch; algorithmic bytes = the blocks' sum (8 B record "
+                 "per element-step), so the launch is bound by fp64 issue and each level's "
+                 "barrier chain, not HBM (roofline_fp64)")
+    out["roofline_fwd"] = None
+    f = out["roofline_fp64"]
+    for k in ("fwd_achieved", "fwd_frac", "fwd_issued_frac"):
+      f[k] = None
+    f["what"] = ("algorithmic fp64 flops of both directions (interior elements) per launch / "
+                 "launch time (adj_*: the one dataflow launch); adj_issued_frac weights each "
+                 "direction's issued/useful lanes (halo) by its flops")
+    out["stream_copy"]["fwd_frac_of_achievable"] = None
+    if out.get("roofline_effective"):
+      out["roofline_effective"].update({"fwd_GBs": None, "fwd_frac": None})
+    out["dataflow"] = {"launches_per_sweep": 1, "blocks_fwd": fchunks, "blocks_adj": chunks,
+                       "work_items": sweep.op.query_sweep(nsteps)[3],
+                       "status": sweep.op.sweep_status()}
+    if out["dataflow"]["status"]:
+      raise RuntimeError("a dataflow work item gave up waiting for a producer")
   if len(set(idx_ranks)) != 1:
     raise RuntimeError(f"refine index differs across ranks: {idx_ranks}")
   if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -816,7 +874,7 @@ def main(argv=None):
     if args.ics == 0:
       out["cpu_baseline_8t"] = cpu_baseline(N, K, cs, threads=8, **kw)
   if rank == 0:
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out, allow_nan=False), flush=True)
   if world > 1:
     import torch.distributed as dist
     dist.destroy_process_group()

@@ -109,6 +109,9 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             workgroup tiles (default 2: tiles of 512*width elements,
  *                             lane-internal faces in registers; bit-identical to 1 at
  *                             equal steps per launch)
+ *   DG_TUNE_REC_SWEEP         1 (default): dg_lserk4_sweep_rec runs forward and adjoint as one
+ *                             dataflow launch where the record shape allows it; 0: as the
+ *                             launch-per-block pair dg_lserk4_fwd_rec + dg_lserk4_adj_rec
  *   DG_TUNE_P_TILE_WIDTH      1 or 2: tile width of the p-enriched estimate (dg_lserk4_adj_p):
  *                             workgroups of 256*value lanes, one element per lane (default 2)
  *   DG_TUNE_P_STEPS_PER_LAUNCH its steps per launch: 1, 2, 4 (default) or 8 (8 needs tile
@@ -120,7 +123,7 @@ enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER =
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
        DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10,
-       DG_TUNE_REC_FWD_TILE_WIDTH = 11 };
+       DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
@@ -241,6 +244,35 @@ int dg_lserk4_fwd_rec(dg_plan* plan, const double* u0, double* uN, double t0, do
                       int nsteps, double* jumps, void* stream);
 int dg_lserk4_adj_rec(dg_plan* plan, double* w, const double* jumps, double t0, double dt,
                       int nsteps, double* eta, int flags, void* stream);
+
+/* The whole sweep pair in one call: dg_lserk4_fwd_rec(u0 -> u^N, jumps) then
+ * dg_lserk4_adj_rec(w, jumps, eta, flags) -- the reference's forward march + adjSolve + errEst
+ * roles (python/Main_finite_difference.py:54-94; utils/One_code.mlx:106-140 for the march) for
+ * a terminal functional.  Where the plan's record shape allows (dg_plan_query_sweep) both
+ * directions run as ONE dataflow launch: the tiles of every block of steps are work items of a
+ * persistent kernel that start as soon as the tiles they read have finished, so the sweep pays
+ * one fill and one drain instead of one per launch.  Results are bit-identical to the two calls.
+ *   u0 (in): u^0.  uN (nullable, must not alias u0 or w): receives u^nsteps.
+ *   w (in/out): the terminal weight dJ/du^N on entry -- or, with DG_SWEEP_TERMINAL_STATE,
+ *     u^N itself (J = |u^N|^2/2; w's content is ignored) -- and w^0 on exit.
+ *   jumps: the record (layout of dg_lserk4_fwd_rec), written and read by the call.
+ *   eta (nullable), flags: DG_ADJ_ETA_ASSIGN / DG_ADJ_ETA_ABS as dg_lserk4_adj_rec.
+ * Scratch: the plan's (block states, indicator partials and the launch's sync words, grown on
+ * the first call of a shape: make that call outside HIP-graph capture). */
+enum { DG_SWEEP_TERMINAL_STATE = 4 };
+int dg_lserk4_sweep_rec(dg_plan* plan, const double* u0, double* uN, double* w, double* jumps,
+                        double t0, double dt, int nsteps, double* eta, int flags, void* stream);
+/* out[0] = 1 if dg_lserk4_sweep_rec runs nsteps as one dataflow launch (else the two launch
+ * chains), out[1] / out[2] = forward / adjoint steps per block, out[3] = work items. */
+int dg_plan_query_sweep(const dg_plan* plan, int nsteps, int64_t out[4]);
+/* Synchronises `stream`; *status = 0, or 1 if a dataflow sweep since the last call gave up
+ * waiting for a producer (a bug: its outputs are garbage; the launch still ended). */
+int dg_sweep_status(dg_plan* plan, int* status, void* stream);
+/* Profiling: with trace non-null (device, 4 uint64 per work item, dg_plan_query_sweep's
+ * out[3] items), every later dataflow sweep of the plan records per item the wall-clock
+ * (100 MHz) times it was taken and its producers were done and it was published, and
+ * (XCC id << 32 | workgroup id).  NULL turns it off. */
+int dg_plan_sweep_trace(dg_plan* plan, uint64_t* trace);
 
 /* ---------------------------------------------------------------------------------------
  * The p-enriched dual-weighted-residual ERROR ESTIMATE.  The reference

@@ -15,8 +15,9 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _run(args, timeout=240):
+def _run(args, timeout=240, env_extra=None):
   env = dict(os.environ)
+  env.update(env_extra or {})
   r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT,
                      capture_output=True, text=True, timeout=timeout, env=env)
   assert r.returncode == 0, r.stderr[-3000:]
@@ -25,9 +26,12 @@ def _run(args, timeout=240):
   return json.loads(lines[0])
 
 
-def test_bench_single_rank_line(gpu):
+@pytest.mark.parametrize("dataflow", [True, False])
+def test_bench_single_rank_line(gpu, dataflow):
+  """The default line (the sweep as one dataflow launch, k_sweep_rp) and the launch-chain
+  line (DG_REC_SWEEP=0: k_step_rp + k_adj_rp, timed per direction)."""
   out = _run(["--K", "65536", "--steps", "3", "--warmup", "2", "--no-converge",
-              "--no-cpu-baseline"])
+              "--no-cpu-baseline"], env_extra={"DG_REC_SWEEP": "1" if dataflow else "0"})
   assert out["n_gpus"] == 1 and out["steps"] == 3 and out["warmup_effective"] == 2
   assert out["unit"] == "DOF-updates/s" and out["value"] > 0
   assert out["roofline"]["bound"] == "hbm" and 0 < out["roofline"]["frac"] < 1
@@ -36,7 +40,15 @@ def test_bench_single_rank_line(gpu):
   assert out["refine_index_ranks"] == [out["refine_index"]]
   assert "flops" not in out and out["dist_world_size"] == 1 and out["collective_backend"] is None
   fp = out["roofline_fp64"]
-  for key in ("adj_frac", "fwd_frac", "adj_issued_frac", "fwd_issued_frac"):
+  keys = ("adj_frac", "fwd_frac", "adj_issued_frac", "fwd_issued_frac")
+  if dataflow:
+    assert out["roofline"]["kernel"].startswith("k_sweep_rp<5")
+    assert out["dataflow"]["status"] == 0 and out["dataflow"]["launches_per_sweep"] == 1
+    assert out["roofline_fwd"] is None and fp["fwd_frac"] is None
+    keys = ("adj_frac", "adj_issued_frac")
+  else:
+    assert "dataflow" not in out and out["roofline"]["kernel"].startswith("k_adj_rp<5")
+  for key in keys:
     assert 0 < fp[key] <= 1, key
   assert fp["adj_issued_frac"] >= fp["adj_frac"] and fp["fwd_halo_factor"] > 1
   assert out["indicator"] == "jump" and "resolved" in out["indicator_resolved"]

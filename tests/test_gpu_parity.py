@@ -402,17 +402,19 @@ def test_adjoint_in_place_on_terminal_snapshot(pkg, gpu, nsteps):
   np.testing.assert_array_equal(host(eta_al), host(eta_sep))
 
 
-def test_ensemble_sweep_graph_matches_eager(pkg, gpu):
-  """The HIP-graph replay of the sweeps (bench path) reproduces the eager sweeps."""
+@pytest.mark.parametrize("record", ["jumps", "snapshots"])
+def test_ensemble_sweep_graph_matches_eager(pkg, gpu, record):
+  """The HIP-graph replay of the sweeps (bench --graph) reproduces the eager sweeps (the jump
+  record's 20-step sweep is one dataflow launch)."""
   import torch
   ens = pkg.ensemble
   mesh = pkg.BaseGalerkin1D(n=4, k=2000)
   dt = mesh.cfl_dt()
-  a = ens.EnsembleSweep(mesh, [0, 1, 2], 10, dt)
-  b = ens.EnsembleSweep(mesh, [0, 1, 2], 10, dt).capture()
+  a = ens.EnsembleSweep(mesh, [0, 1, 2], 20, dt, record=record)
+  b = ens.EnsembleSweep(mesh, [0, 1, 2], 20, dt, record=record).capture()
+  assert b.dataflow == (record == "jumps")
   pa = a.run().clone()
-  b.forward_graph()
-  b.adjoint_graph()
+  b.sweep_graph()
   pb = b.reduce().clone()
   torch.cuda.synchronize()
   np.testing.assert_array_equal(host(pa), host(pb))

@@ -1,0 +1,197 @@
+"""The dataflow sweep (dg_lserk4_sweep_rec, csrc/dg_sweep.hip): forward and adjoint record
+sweeps as ONE launch whose work items are the tiles of every block of steps.
+
+Bars:
+  * bit-identical to the launch-per-block pair (dg_lserk4_fwd_rec + dg_lserk4_adj_rec, the
+    same tile arithmetic and steps per block) in u^N, the record, w^0 and eta -- for every Np
+    the pair tiles run at 1024 elements, 10- and 20-step forward blocks, 1 to 4 adjoint
+    blocks, batches with trajectory edges inside tiles, both inflow variants, a refined mesh,
+    every indicator mode and a caller-supplied terminal weight;
+  * repeated launches (the kernel re-arms its own queue and epochs) and HIP-graph replays give
+    the same bits; a launch beside a concurrent bandwidth-heavy kernel (uneven load on the
+    hand-offs, cdna_hip_programming.md §6 Guideline 16 pitfall 3) too;
+  * no launch gives up waiting for a producer (dg_sweep_status);
+  * shapes the dataflow launch does not cover fall back to the two launch chains (query).
+The oracle comparison of this path at full size is tests/test_gpu_full_size.py (the bench's
+EnsembleSweep runs it).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def host(t):
+  return t.detach().cpu().numpy()
+
+
+def noisy_sine(op, seed, batch):
+  import torch
+  rng = np.random.default_rng(seed)
+  u0 = op.new_field()
+  op.init_sine(rng.uniform(0.5, 1.5, batch), rng.integers(1, 5, batch).astype(float),
+               rng.uniform(0, 6, batch), out=u0)
+  gen = torch.Generator(device=u0.device).manual_seed(seed)
+  u0 += 0.1 * torch.randn(u0.shape, dtype=u0.dtype, device=u0.device, generator=gen)
+  return u0
+
+
+def run_sweep(op, u0, dt, nsteps, dataflow, eta_assign=True, eta_abs=False, eta_init=None,
+              with_eta=True, terminal=None):
+  """One sweep_rec call; returns (uN, rec, w, eta) as host arrays."""
+  import torch
+  op.tune(rec_sweep=1 if dataflow else 0)
+  rec = op.new_jumps(nsteps)
+  rec.fill_(float("nan"))
+  uN = op.new_field()
+  w = op.new_field() if terminal is None else terminal.clone()
+  eta = None
+  if with_eta:
+    eta = (torch.full((op.ktot,), float("nan"), dtype=torch.float64, device=op.device)
+           if eta_init is None else eta_init.clone())
+  op.sweep_rec(u0, rec, w, 0.0, dt, nsteps, uN=uN, eta=eta, eta_assign=eta_assign,
+               eta_abs=eta_abs, terminal_state=terminal is None)
+  torch.cuda.synchronize()
+  out = (host(uN), host(rec), host(w), None if eta is None else host(eta))
+  if dataflow:
+    assert op.sweep_status() == 0, "a work item gave up waiting for a producer"
+  return out
+
+
+def assert_same(a, b, what):
+  for name, x, y in zip(("u^N", "record", "w^0", "eta"), a, b):
+    if x is None and y is None:
+      continue
+    np.testing.assert_array_equal(x, y, err_msg=f"{what}: {name}")
+
+
+@pytest.mark.parametrize("N,K,batch,fsteps,nsteps,inflow,refined", [
+    (4, 5000, 1, 20, 20, "a", False),      # the bench's shape: forward 20, adjoint 10 + 10
+    (4, 5000, 1, 10, 20, "a", False),      # forward 10 + 10
+    (4, 3000, 3, 20, 40, "a2", False),    # trajectory edges inside tiles, 2 + 4 blocks
+    (4, 2500, 2, 10, 30, "a", False),      # 3 + 3 blocks
+    (1, 4000, 1, 20, 20, "a", False),
+    (2, 1500, 2, 10, 10, "a", False),      # one block each way
+    (3, 2000, 1, 20, 20, "zero", False),
+    (5, 2000, 2, 20, 20, "a", False),
+    (6, 1200, 1, 10, 20, "a", False),
+    (7, 1100, 1, 20, 20, "a", False),
+    (4, 3000, 2, 20, 20, "a", True),       # refined (non-uniform metric)
+    (4, 700, 1, 20, 20, "a", False),       # fewer elements than one tile's output
+])
+def test_dataflow_equals_launch_chains(pkg, gpu, N, K, batch, fsteps, nsteps, inflow, refined):
+  v_x = np.linspace(0.0, 1.0, K + 1)
+  if refined:
+    for k in (3, 900, 901, K - 1):
+      v_x = np.insert(v_x, k + 1, 0.5 * (v_x[k] + v_x[k + 1]))
+  mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+  op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
+  assert op.uniform != refined
+  op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=fsteps)
+  on, msf, msa, items = op.query_sweep(nsteps)
+  assert on and (msf, msa) == (fsteps, 10) and items > 0
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 11 + N, batch)
+  for assign, absval in ((True, False), (True, True)):
+    ref = run_sweep(op, u0, dt, nsteps, False, assign, absval)
+    got = run_sweep(op, u0, dt, nsteps, True, assign, absval)
+    assert_same(got, ref, f"N={N} K={K} batch={batch} {fsteps}/{nsteps} assign={assign} abs={absval}")
+  assert np.isfinite(ref[3]).all() and np.abs(ref[3]).max() > 0
+
+
+def test_dataflow_indicator_modes_and_terminal_weight(pkg, gpu):
+  """eta accumulated onto caller values, no eta, a caller terminal weight (in place over 2
+  blocks, through a copy with one block)."""
+  import torch
+  N, K, nsteps = 4, 2600, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh, batch=2)
+  op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=20)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 3, 2)
+  init = torch.linspace(-1.0, 1.0, op.ktot, dtype=torch.float64, device=gpu)
+  for kw in (dict(eta_assign=False, eta_init=init), dict(eta_assign=False, eta_abs=True,
+                                                         eta_init=init),
+             dict(with_eta=False)):
+    ref = run_sweep(op, u0, dt, nsteps, False, **kw)
+    got = run_sweep(op, u0, dt, nsteps, True, **kw)
+    assert_same(got, ref, str({k: v for k, v in kw.items() if k != "eta_init"}))
+  g = noisy_sine(op, 9, 2)  # an arbitrary terminal weight dJ/du^N
+  for n in (20, 10):
+    ref = run_sweep(op, u0, dt, n, False, terminal=g)
+    got = run_sweep(op, u0, dt, n, True, terminal=g)
+    assert_same(got, ref, f"terminal weight, nsteps={n}")
+
+
+def test_dataflow_repeats_graphs_and_uneven_load(pkg, gpu):
+  """Back-to-back launches (self re-armed queue, epochs), HIP-graph replays and launches
+  racing a bandwidth-heavy copy on another stream all give the same bits."""
+  import torch
+  N, K, nsteps = 4, 60000, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=20, rec_sweep=1)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 21, 1)
+  ref = run_sweep(op, u0, dt, nsteps, False)
+  rec, uN, w = op.new_jumps(nsteps), op.new_field(), op.new_field()
+  eta = torch.zeros(op.ktot, dtype=torch.float64, device=gpu)
+
+  def sweep():
+    op.sweep_rec(u0, rec, w, 0.0, dt, nsteps, uN=uN, eta=eta, eta_assign=True)
+
+  def check(what):
+    torch.cuda.synchronize()
+    assert_same((host(uN), host(rec), host(w), host(eta)), ref, what)
+
+  for i in range(5):
+    sweep()
+  check("5 back-to-back launches")
+  # HIP graph (the first call above allocated the scratch outside capture)
+  side = torch.cuda.Stream()
+  side.wait_stream(torch.cuda.current_stream())
+  with torch.cuda.stream(side):
+    sweep()
+  torch.cuda.current_stream().wait_stream(side)
+  torch.cuda.synchronize()
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    sweep()
+  for i in range(3):
+    w.zero_()
+    eta.zero_()
+    g.replay()
+  check("graph replays")
+  # uneven load: a 1 GiB stream copy on another stream while the sweeps run
+  big = torch.empty(1 << 27, dtype=torch.float64, device=gpu)
+  dst = torch.empty_like(big)
+  copy_stream = torch.cuda.Stream()
+  for i in range(3):
+    with torch.cuda.stream(copy_stream):
+      pkg.operators.stream_copy(big, dst)
+    sweep()
+    check(f"beside a concurrent copy ({i})")
+  assert op.sweep_status() == 0
+
+
+def test_dataflow_fallbacks(pkg, gpu):
+  """Shapes the dataflow launch does not cover run the launch chains with the same results:
+  nsteps not a multiple of the blocks, more than 40 steps, 512-element tiles, the switch off."""
+  mesh = pkg.BaseGalerkin1D(n=4, k=1500)
+  op = pkg.operators.DGAdvection1D(mesh)
+  op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=20)
+  assert op.query_sweep(20)[0]
+  assert not op.query_sweep(15)[0]
+  assert not op.query_sweep(60)[0]
+  assert not op.query_sweep(0)[0]
+  op.tune(rec_sweep=0)
+  assert not op.query_sweep(20)[0]
+  op.tune(rec_sweep=1, rec_tile_width=1, rec_steps_per_launch=10)
+  assert not op.query_sweep(20)[0]
+  op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=20)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 4, 1)
+  for n in (15, 7):
+    ref = run_sweep(op, u0, dt, n, False)
+    got = run_sweep(op, u0, dt, n, True)  # the fallback inside sweep_rec
+    assert_same(got, ref, f"fallback nsteps={n}")
