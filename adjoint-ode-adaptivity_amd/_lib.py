@@ -63,6 +63,8 @@ SIGNATURES = {
                                  _i32, _vp]),
     "dg_lserk4_sweep_rec": (_i32, [_vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                    _i32, _vp, _i32, _vp]),
+    "dg_lserk4_sweep_refine": (_i32, [_vp, _vp, _vp, _vp, _vp, ctypes.c_double,
+                                      ctypes.c_double, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "dg_plan_query_sweep": (_i32, [_vp, _i32, _vp]),
     "dg_sweep_status": (_i32, [_vp, ctypes.POINTER(_i32), _vp]),
     "dg_plan_sweep_trace": (_i32, [_vp, _vp]),
@@ -75,6 +77,7 @@ SIGNATURES = {
     "dg_argmax": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp]),
     "dg_argmax_ex": (_i32, [_vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "dg_stream_copy": (_i32, [_vp, _vp, _i64, _vp]),
+    "dg_host_alias": (_i32, [_vp, ctypes.POINTER(_vp)]),
     "dg_sum_rows": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "dg_init_sine": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "dg_time_march": (_i32, [_i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp, ctypes.c_double,

@@ -1070,16 +1070,16 @@ inline int chunk(const dg_plan* p, int left) {
 
 // The dataflow sweep's blocks for `nsteps` steps (dg_sweep.hip): true with the forward /
 // adjoint steps per block when the plan runs it -- pair tiles of 1024 elements in both
-// directions, the record shape's 10- or 20-step forward and 10-step adjoint launches as its
-// blocks, nsteps a multiple of both and at most sweep_max_steps() -- else false (the
+// directions, the record shape's 5-, 10- or 20-step forward and 5- or 10-step adjoint launches
+// as its blocks, nsteps a multiple of both and at most sweep_max_steps() -- else false (the
 // launch-per-block pair runs, with the same results).
 bool sweep_shape(const dg_plan* p, int nsteps, int* msf, int* msa) {
   const int f = rec_msteps_fwd(p), a = rec_msteps(p);
   *msf = f;
   *msa = a;
   return p->rec_sweep && rec_pairs(p) && rec_fwd_width(p) == 2 && p->rec_tile_width == 2 &&
-         (f == 10 || f == 20) && a == 10 && nsteps > 0 && nsteps % f == 0 && nsteps % a == 0 &&
-         nsteps <= sweep_max_steps();
+         (f == 5 || f == 10 || f == 20) && (a == 5 || a == 10) && nsteps > 0 &&
+         nsteps % f == 0 && nsteps % a == 0 && nsteps <= sweep_max_steps();
 }
 
 // The plan's dataflow scratch: a control region of sync words and flags (zeroed once, then
@@ -1686,9 +1686,16 @@ int dg_lserk4_adj_rec(dg_plan* p, double* w, const double* jumps, double t0, dou
   return DG_OK;
 }
 
-int dg_lserk4_sweep_rec(dg_plan* p, const double* u0, double* uN, double* w, double* jumps,
-                        double t0, double dt, int nsteps, double* eta, int flags, void* stream) {
+}  // extern "C"
+
+namespace {
+// dg_lserk4_sweep_rec, and with `idx` non-null also the refine decision dg_argmax_ex(eta,
+// |.|) -- fused into the dataflow launch, or a separate reduction after the launch chains.
+int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* jumps,
+                   double t0, double dt, int nsteps, double* eta, int flags, int64_t* idx,
+                   double* value, int64_t* nonfinite, void* stream) {
   if (!p || !u0 || !w || (!jumps && nsteps > 0)) return fail(DG_ERR_ARG, "null argument");
+  if (idx && !eta) return fail(DG_ERR_ARG, "the refine decision needs eta");
   if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
   if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS | DG_SWEEP_TERMINAL_STATE))
     return fail(DG_ERR_ARG, "unknown flags");
@@ -1715,7 +1722,9 @@ int dg_lserk4_sweep_rec(dg_plan* p, const double* u0, double* uN, double* w, dou
     }
     if (const int rc = dg_lserk4_fwd_rec(p, u0, fin, t0, dt, nsteps, jumps, stream)) return rc;
     if (term && fin != w) HIP_TRY(hipMemcpyAsync(w, fin, fbytes, hipMemcpyDeviceToDevice, st));
-    return dg_lserk4_adj_rec(p, w, jumps, t0, dt, nsteps, eta, aflags, stream);
+    if (const int rc = dg_lserk4_adj_rec(p, w, jumps, t0, dt, nsteps, eta, aflags, stream))
+      return rc;
+    return idx ? dg_argmax_ex(p, eta, p->ktot, 1, idx, value, nonfinite, stream) : DG_OK;
   }
   const int nbF = nsteps / msf, nbA = nsteps / msa;
   const int64_t items = sweep_items(p, msf, msa, nsteps);
@@ -1726,7 +1735,9 @@ int dg_lserk4_sweep_rec(dg_plan* p, const double* u0, double* uN, double* w, dou
   const int wcopy = (!term && nbA == 1) ? 1 : 0;
   const int nfields = (nbF - 1) + (uN ? 0 : 1) + (nbA - 1) + wcopy;
   const int nparts = eta ? nbA - 1 : 0;
-  const size_t bytes = sync_bytes + fbytes * size_t(nfields) + sizeof(double) * size_t(p->ktot) * size_t(nparts);
+  const int64_t am_parts = idx ? sweep_tiles_adj(p, msa) : 0;
+  const size_t bytes = sync_bytes + fbytes * size_t(nfields) +
+                       sizeof(double) * size_t(p->ktot) * size_t(nparts) + 16 * size_t(am_parts);
   char* data = nullptr;
   if (const int rc = sweep_scratch(p, sync_bytes, bytes - sync_bytes, st, &data)) return rc;
   if (p->sweep_items != items) {
@@ -1754,10 +1765,35 @@ int dg_lserk4_sweep_rec(dg_plan* p, const double* u0, double* uN, double* w, dou
   b.rec = jumps;
   b.eta = eta;
   b.part = nparts ? fld + field * next : nullptr;
+  double* am = fld + field * next + p->ktot * nparts;
+  b.am_idx = idx;
+  b.am_val = value;
+  b.am_nf = nonfinite;
+  b.am_pv = idx ? am : nullptr;
+  b.am_pi = idx ? reinterpret_cast<int64_t*>(am + am_parts) : nullptr;
   const int mode = eta ? (kEtaOn | ((aflags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
                           ((aflags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
                        : 0;
-  return sweep_launch_rec(p, msf, b, t0, dt, nsteps, mode, st);
+  return sweep_launch_rec(p, msf, msa, b, t0, dt, nsteps, mode, st);
+}
+}  // namespace
+
+extern "C" {
+
+int dg_lserk4_sweep_rec(dg_plan* p, const double* u0, double* uN, double* w, double* jumps,
+                        double t0, double dt, int nsteps, double* eta, int flags, void* stream) {
+  return sweep_rec_impl(p, u0, uN, w, jumps, t0, dt, nsteps, eta, flags, nullptr, nullptr,
+                        nullptr, stream);
+}
+
+int dg_lserk4_sweep_refine(dg_plan* p, const double* u0, double* uN, double* w, double* jumps,
+                           double t0, double dt, int nsteps, double* eta, int flags,
+                           int64_t* idx, double* value, int64_t* nonfinite_count,
+                           void* stream) {
+  if (!idx) return fail(DG_ERR_ARG, "null argument");
+  if (nsteps < 1) return fail(DG_ERR_ARG, "the refine decision needs nsteps >= 1");
+  return sweep_rec_impl(p, u0, uN, w, jumps, t0, dt, nsteps, eta, flags, idx, value,
+                        nonfinite_count, stream);
 }
 
 int dg_plan_query_sweep(const dg_plan* p, int nsteps, int64_t out[4]) {

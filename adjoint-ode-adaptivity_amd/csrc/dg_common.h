@@ -590,16 +590,22 @@ int wave_launch_step(const dg_plan* p, int ms, const double* in, double* snap, d
 // W[nbA] the caller's w); part: (nbA - 1) rows of ktot indicator partials; sync: the
 // sweep_sync_words() control words followed by one flag per item.
 struct SweepBufs {
-  double* U[5];
-  double* W[5];
+  double* U[9];
+  double* W[9];
   double* rec;
   double* eta;
   double* part;
   uint32_t* sync;
+  int64_t* am_idx;  // nullable: fused refine decision (dg_argmax_ex of |eta|)
+  double* am_val;
+  int64_t* am_nf;
+  double* am_pv;    // partial winners, one per last-block tile
+  int64_t* am_pi;
 };
 int64_t sweep_items(const dg_plan* p, int msf, int msa, int nsteps);
-int sweep_launch_rec(dg_plan* p, int msf, const SweepBufs& b, double t0, double dt, int nsteps,
-                     int mode, hipStream_t st);
+int64_t sweep_tiles_adj(const dg_plan* p, int msa);
+int sweep_launch_rec(dg_plan* p, int msf, int msa, const SweepBufs& b, double t0, double dt,
+                     int nsteps, int mode, hipStream_t st);
 int sweep_sync_words();
 int sweep_max_steps();
 int sweep_err_word();

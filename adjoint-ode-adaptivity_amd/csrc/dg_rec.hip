@@ -64,7 +64,7 @@ __global__ __launch_bounds__(64 * NW) void k_adj_rp(const double* __restrict__ w
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.c.xcd);
   constexpr int H = RpHalo<MS>::A;
   const int64_t e0 = tile * (G::T - 2 * H) - H;
-  const EtaSink es{eta, nullptr, nullptr, 0, 0, args.has_eta};
+  EtaSink es{eta, nullptr, nullptr, 0, 0, args.has_eta, false, 0.0, 0};
   if (edge_tile(e0, G::T, args.c.ktot, args.c.K))
     rp_adj_tile<NP, UNI, NW, E, MS, true, false>(lds, tile, win, wout, rec, es, scale, args.c,
                                                  args.n0);

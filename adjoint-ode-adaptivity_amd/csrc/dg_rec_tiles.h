@@ -537,7 +537,21 @@ struct EtaSink {
   int64_t part_ld;
   int32_t nparts;      // partial rows to combine (last block)
   int32_t mode;        // kEta* bits; 0: no indicator
+  // WT, last block: the lane's best (|eta|, element) of its final values under numpy's
+  // argmax order (am_better), for the dataflow sweep's fused refine decision
+  bool argmax;
+  double bv;
+  int64_t bi;
 };
+
+// numpy.argmax order: NaN is the maximum, ties go to the lowest index (a strict total order
+// on (value, index), so any reduction tree gives the same winner; dg_argmax's rule).
+__device__ __forceinline__ bool am_better(double va, int64_t ia, double vb, int64_t ib) {
+  const bool na = isnan(va), nb = isnan(vb);
+  if (na != nb) return na;
+  if (!na && va != vb) return va > vb;
+  return ia < ib;
+}
 
 // Adjoint: MS reverse steps st = MS-1..0 of the tile, each
 //   eta += DWR(u^{n0+st+1}'s recorded jumps, w^{n0+st+1});  w^{n0+st} = P(z^T) w^{n0+st+1}
@@ -550,7 +564,7 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
                                             const double* __restrict__ win,
                                             double* __restrict__ wout,
                                             const double* __restrict__ rec,
-                                            const EtaSink& es,
+                                            EtaSink& es,
                                             const double* __restrict__ scale,
                                             const RpOp<NP>& c, int64_t n0) {
   using G = RpGeo<NP, NW, E>;
@@ -743,6 +757,10 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
           }
           if (has_eta & kEtaAbs) v = fabs(v);
           wt_st8(ro, o, v);
+          if (es.argmax && am_better(fabs(v), El[m].e, es.bv, es.bi)) {
+            es.bv = fabs(v);
+            es.bi = El[m].e;
+          }
         }
       }
     } else {

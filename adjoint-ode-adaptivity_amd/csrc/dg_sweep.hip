@@ -42,9 +42,10 @@ using namespace dgk;
 using namespace dgr;
 
 constexpr int kSweepMaxSteps = 40;   // steps per sweep (the forward blocks' constants are kernargs)
-constexpr int kSweepMaxBlocks = 4;   // blocks per direction (kSweepMaxSteps / 10)
-// control words (uint32 index): a 64-bit take counter, the error word, then one flag per item
-constexpr int kSyncHead = 0, kSyncErr = 2, kSyncFlags = 16;
+constexpr int kSweepMaxBlocks = 8;   // blocks per direction (kSweepMaxSteps / 5)
+// control words (uint32 index): a 64-bit take counter, the error word, a 64-bit arrival
+// counter of the fused refine decision, then one flag per item
+constexpr int kSyncHead = 0, kSyncErr = 2, kSyncArrive = 4, kSyncFlags = 16;
 constexpr int kSweepSpinLimit = 1 << 20;
 #ifndef DG_SWEEP_WAVES
 #define DG_SWEEP_WAVES 5
@@ -62,6 +63,11 @@ template <int NP, int MSF> struct SweepArgs {
   uint32_t* sync;                  // kSync* words, then one flag per item
   uint64_t* trace;                 // nullable: per item {dequeued, producers done, published,
                                    // XCC id << 32 | workgroup id} (wall clock, 100 MHz)
+  int64_t* am_idx;                 // nullable: the fused refine decision, dg_argmax_ex(|eta|)
+  double* am_val;
+  int64_t* am_nf;
+  double* am_pv;                   // per last-block tile: its (|eta|, element) winner
+  int64_t* am_pi;
   int32_t nbF, nbA, nTF, nTA;
   int32_t nsteps;
   int32_t mode;                    // kEta* bits (0: no indicator)
@@ -93,6 +99,41 @@ __device__ __forceinline__ void sweep_wait(const uint32_t* flags, int nd, uint32
   }
 }
 
+// Winner of (v, i) over the 512-lane workgroup under am_better; valid in thread 0.  sv / si:
+// 8 LDS slots of the caller's own (not aliased with a tile image another wave may read).
+__device__ __forceinline__ void wg_argmax(double& v, int64_t& i, double* sv, int64_t* si) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(v, off);
+    const int64_t oi = __shfl_xor(i, off);
+    if (am_better(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sv[wv] = v;
+    si[wv] = i;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 1; k < 8; ++k)
+      if (am_better(sv[k], si[k], v, i)) {
+        v = sv[k];
+        i = si[k];
+      }
+}
+
+__device__ __forceinline__ void st8_agent(void* p, uint64_t bits) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), bits, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld8_agent(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NP, bool UNI, int MSF, int MSA>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WAVES))) void k_sweep_rp(
     SweepArgs<NP, MSF> a) {
@@ -101,7 +142,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
   constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
   constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MSF * 6 + 1];
-  __shared__ uint32_t s_item, s_epoch;
+  __shared__ uint32_t s_item, s_epoch, s_last;
+  __shared__ double s_av[8];
+  __shared__ int64_t s_ai[8];
   uint32_t* sync = a.sync;
   uint32_t* flags = sync + kSyncFlags;
   const int tid = threadIdx.x;
@@ -185,6 +228,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
       es.part_ld = ktot;
       es.nparts = lastb ? a.nbA - 1 : 0;
       es.mode = a.mode;
+      es.argmax = lastb && a.am_idx != nullptr;
+      es.bv = -INFINITY;  // the weakest candidate (dg_argmax's convention)
+      es.bi = INT64_MAX;
       const int64_t n0 = int64_t(a.nsteps) - int64_t(blk + 1) * MSA;
       if (edge_tile(e0, G::T, ktot, a.c.K))
         rp_adj_tile<NP, UNI, NW, E, MSA, true, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
@@ -192,11 +238,49 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
       else
         rp_adj_tile<NP, UNI, NW, E, MSA, false, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
                                                       a.scale, a.c, n0);
+      if (es.argmax) {  // the tile's winner, a hand-off to the last arriving tile
+        wg_argmax(es.bv, es.bi, s_av, s_ai);
+        if (tid == 0) {
+          st8_agent(a.am_pv + j, __builtin_bit_cast(uint64_t, es.bv));
+          st8_agent(a.am_pi + j, uint64_t(es.bi));
+        }
+      }
     }
     // publish: every wave's write-through stores have completed, then one flag store
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) st_agent(flags + item, epoch);
+    if (!fwd && blk == nbA - 1 && a.am_idx != nullptr) {
+      // Fused refine decision: the last block's tiles arrive on a counter that grows by nTA
+      // per launch; the one whose add completes a launch's count reduces the nTA winners
+      // (published above, write-through, drained before the add) with sc1 loads.
+      if (tid == 0) {
+        const uint64_t old = __hip_atomic_fetch_add(
+            reinterpret_cast<uint64_t*>(sync + kSyncArrive), uint64_t(1), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        s_last = ((old + 1) % uint64_t(nTA)) == 0 ? 1u : 0u;
+      }
+      __syncthreads();
+      if (s_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double v = -INFINITY;
+        int64_t i = INT64_MAX;
+        for (int q = tid; q < nTA; q += 512) {
+          const double pv = __builtin_bit_cast(double, ld8_agent(a.am_pv + q));
+          const int64_t pi = int64_t(ld8_agent(a.am_pi + q));
+          if (am_better(pv, pi, v, i)) {
+            v = pv;
+            i = pi;
+          }
+        }
+        wg_argmax(v, i, s_av, s_ai);
+        if (tid == 0) {
+          a.am_idx[0] = i;
+          if (a.am_val) a.am_val[0] = v;
+          if (a.am_nf && !isfinite(v)) a.am_nf[0] += 1;
+        }
+      }
+    }
     if (a.trace && tid == 0) {
       uint32_t xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -232,6 +316,11 @@ int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int 
   a.scale = p->d_scale;
   a.sync = b.sync;
   a.trace = p->sweep_trace;
+  a.am_idx = b.am_idx;
+  a.am_val = b.am_val;
+  a.am_nf = b.am_nf;
+  a.am_pv = b.am_pv;
+  a.am_pi = b.am_pi;
   a.nbF = nbF;
   a.nbA = nbA;
   using G = RpGeo<NP, 8, 2>;
@@ -246,14 +335,26 @@ int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int 
   return DG_OK;
 }
 
+template <int NP, bool UNI>
+int sweep_shape_launch(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0,
+                       double dt, int nsteps, int mode, hipStream_t st) {
+  if (msa == 10) {
+    if (msf == 20) return sweep_launch<NP, UNI, 20, 10>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 10) return sweep_launch<NP, UNI, 10, 10>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 5) return sweep_launch<NP, UNI, 5, 10>(p, b, t0, dt, nsteps, mode, st);
+  } else if (msa == 5) {
+    if (msf == 20) return sweep_launch<NP, UNI, 20, 5>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 10) return sweep_launch<NP, UNI, 10, 5>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 5) return sweep_launch<NP, UNI, 5, 5>(p, b, t0, dt, nsteps, mode, st);
+  }
+  return fail(DG_ERR_ARG, "dataflow sweep: unsupported steps per block");
+}
+
 template <int NP>
-int sweep_np(dg_plan* p, int msf, const dgk::SweepBufs& b, double t0, double dt, int nsteps,
-             int mode, hipStream_t st) {
-  if (msf == 20)
-    return p->uniform ? sweep_launch<NP, true, 20, 10>(p, b, t0, dt, nsteps, mode, st)
-                      : sweep_launch<NP, false, 20, 10>(p, b, t0, dt, nsteps, mode, st);
-  return p->uniform ? sweep_launch<NP, true, 10, 10>(p, b, t0, dt, nsteps, mode, st)
-                    : sweep_launch<NP, false, 10, 10>(p, b, t0, dt, nsteps, mode, st);
+int sweep_np(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0, double dt,
+             int nsteps, int mode, hipStream_t st) {
+  return p->uniform ? sweep_shape_launch<NP, true>(p, msf, msa, b, t0, dt, nsteps, mode, st)
+                    : sweep_shape_launch<NP, false>(p, msf, msa, b, t0, dt, nsteps, mode, st);
 }
 
 }  // namespace
@@ -267,10 +368,14 @@ int64_t sweep_items(const dg_plan* p, int msf, int msa, int nsteps) {
   return int64_t(nsteps / msf) * nTF + int64_t(nsteps / msa) * nTA;
 }
 
-int sweep_launch_rec(dg_plan* p, int msf, const SweepBufs& b, double t0, double dt,
+int64_t sweep_tiles_adj(const dg_plan* p, int msa) {
+  return grid_for(p->ktot, 1024 - 2 * ((msa * 5 + 1) & ~1));
+}
+
+int sweep_launch_rec(dg_plan* p, int msf, int msa, const SweepBufs& b, double t0, double dt,
                      int nsteps, int mode, hipStream_t st) {
   int rc = DG_OK;
-  DG_DISPATCH_NP(p->NP, rc = sweep_np<NP>(p, msf, b, t0, dt, nsteps, mode, st));
+  DG_DISPATCH_NP(p->NP, rc = sweep_np<NP>(p, msf, msa, b, t0, dt, nsteps, mode, st));
   return rc;
 }
 

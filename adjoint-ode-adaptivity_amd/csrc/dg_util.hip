@@ -51,3 +51,17 @@ extern "C" int dg_stream_copy(const double* src, double* dst, int64_t n, void* s
     HIP_TRY(hipMemcpyAsync(dst + n - 1, src + n - 1, sizeof(double), hipMemcpyDeviceToDevice, st));
   return DG_OK;
 }
+
+// The device address of page-locked host memory (hipHostGetDevicePointer): kernels can then
+// write small results (the refine decision) straight to the host, with no copy launch.
+extern "C" int dg_host_alias(void* host, void** device) {
+  if (!host || !device) return fail(DG_ERR_ARG, "null argument");
+  *device = nullptr;
+  void* d = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&d, host, 0);
+  if (e != hipSuccess || !d)
+    return fail(DG_ERR_ARG, std::string("not mapped page-locked host memory: ") +
+                                hipGetErrorString(e));
+  *device = d;
+  return DG_OK;
+}

@@ -156,6 +156,19 @@ class EnsembleSweep:
       self.forward()
       self.adjoint()
 
+  def sweep_refine(self, reducer, idx=None, value=None):
+    """``sweep`` plus the refine decision into ``reducer`` (index, value, non-finite count:
+    the DeviceReducer state) in ONE dg_lserk4_sweep_refine call -- for a single trajectory on
+    a single rank, whose indicator is the whole mean (Main_width_ref.py:479 with one IC); the
+    dataflow launch reduces the argmax in its last tiles.  ``idx`` / ``value``: other
+    destinations for the index and value (e.g. ``operators.host_alias`` addresses of pinned
+    host memory: the decision lands on the host with no copy launch)."""
+    if self.record != "jumps" or self.batch != 1:
+      raise ValueError("sweep_refine: one trajectory with the jump record")
+    self.op.sweep_refine(self.u0, self.jumps, self.w, 0.0, self.dt, self.nsteps, self.eta,
+                         reducer.idx if idx is None else idx,
+                         reducer.value if value is None else value, reducer.nonfinite)
+
   def capture(self):
     """Capture the sweep as HIP graphs (replayed by sweep_graph, or forward_graph /
     adjoint_graph for the two halves of the snapshot pair): the per-launch host work

@@ -332,6 +332,32 @@ class DGAdvection1D:
     _lib.check(rc, "dg_lserk4_sweep_rec")
     return w, eta
 
+  def sweep_refine(self, u0, jumps, w, t0, dt, nsteps, eta, idx, value=None, nonfinite=None,
+                   uN=None, eta_assign=True, eta_abs=True, terminal_state=True):
+    """``sweep_rec`` + the refine decision ``argmax_ex(eta, use_abs=True)`` in one call
+    (dg_lserk4_sweep_refine): in the dataflow launch the last adjoint tiles reduce the argmax
+    themselves.  ``idx`` / ``nonfinite`` (CUDA int64, 1) and ``value`` (CUDA float64, 1) as
+    for ``argmax_ex``."""
+    def p1(t, dtype, name):
+      if t is None:
+        return None
+      if isinstance(t, int):  # a device address (host_alias of pinned host memory)
+        return ctypes.c_void_p(t)
+      if not t.is_cuda or t.dtype != dtype or t.numel() < 1:
+        raise TypeError(f"{name} must be a CUDA {dtype} tensor or a device address")
+      return ctypes.c_void_p(t.data_ptr())
+    flags = ((_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) |
+             (_lib.DG_ADJ_ETA_ABS if eta_abs else 0) |
+             (_lib.DG_SWEEP_TERMINAL_STATE if terminal_state else 0))
+    un_p = None if uN is None else self._field(uN, "uN")
+    rc = self._lib.dg_lserk4_sweep_refine(
+        self._plan, self._field(u0, "u0"), un_p, self._field(w, "w"), self._jumps(jumps, nsteps),
+        float(t0), float(dt), int(nsteps), self._field(eta, "eta", self.ktot), int(flags),
+        p1(idx, torch.int64, "idx"), p1(value, torch.float64, "value"),
+        p1(nonfinite, torch.int64, "nonfinite"), _stream(self.device))
+    _lib.check(rc, "dg_lserk4_sweep_refine")
+    return idx
+
   def query_sweep(self, nsteps):
     """(dataflow, forward steps per block, adjoint steps per block, work items) of
     ``sweep_rec`` for an ``nsteps`` sweep; dataflow False: the two launch chains run."""
@@ -493,6 +519,18 @@ class DWREstimate:
 
   def close(self):
     self.hi.close()
+
+
+def host_alias(t):
+  """The device address of a pinned (page-locked, mapped) host tensor's storage, for kernels
+  that write small results straight to the host (dg_host_alias); None if it is not mapped."""
+  if t.is_cuda or not t.is_pinned():
+    return None
+  lib = _lib.load()
+  d = ctypes.c_void_p()
+  if lib.dg_host_alias(ctypes.c_void_p(t.data_ptr()), ctypes.byref(d)) != _lib.DG_OK:
+    return None
+  return int(d.value) if d.value else None
 
 
 def stream_copy(src, dst):

@@ -567,12 +567,36 @@ def main(argv=None):
   stream = torch.cuda.current_stream(dev)
   res_host = torch.zeros(2, dtype=torch.int64).pin_memory()  # refine index, value bits
   # The jump record's sweep as ONE dataflow launch (dg_lserk4_sweep_rec, csrc/dg_sweep.hip)
-  # where the plan's shape allows: forward and adjoint are then not separately timeable.
+  # where the plan's shape allows: forward and adjoint are then not separately timeable.  With
+  # one trajectory on one rank the indicator is the whole mean, so the refine decision is
+  # reduced inside the same launch (dg_lserk4_sweep_refine).
   dataflow = sweep.dataflow
+  fused_refine = (dataflow and world == 1 and sweep.batch == 1 and not args.gather_ics
+                  and not args.graph)
+  # The refine index (the mesh split's input) and the indicator there go to the host in one
+  # async copy into pinned memory, read after the timed region has synced.  (The copy on a
+  # side stream, with the next step waiting for it before rewriting the state, measured
+  # ~30 us slower per step: the cross-stream event round trip, profiles/r03/sweep/ab5.)
+  def copy_result():
+    res_host.copy_(reducer.state[0:2], non_blocking=True)
+
+  # The fused refine decision writes index and value straight into the pinned result buffer
+  # (its device alias): no copy launch per step.
+  res_alias = pkg.operators.host_alias(res_host) if fused_refine else None
 
   def one_step(ev=None):
     if ev:
       ev[0].record(stream)
+    if fused_refine:
+      if res_alias is not None:
+        sweep.sweep_refine(reducer, idx=res_alias, value=res_alias + 8)
+      else:
+        sweep.sweep_refine(reducer)
+      if ev:
+        ev[2].record(stream)
+      if res_alias is None:
+        copy_result()
+      return
     if dataflow:
       sweep.sweep_graph() if args.graph else sweep.sweep()
       if ev:
@@ -581,7 +605,7 @@ def main(argv=None):
       ens.gather_indicator(partial, n_total, reducer)
       if args.gather_ics:
         ens.gather_per_ic(sweep.per_ic(), n_total)
-      res_host.copy_(reducer.state[0:2], non_blocking=True)
+      copy_result()
       return
     sweep.forward_graph() if args.graph else sweep.forward()
     if ev:
@@ -599,7 +623,7 @@ def main(argv=None):
       ens.gather_per_ic(sweep.per_ic(), n_total)
     # The refine index (the mesh split's input) and the indicator there go to the host in
     # one async copy into pinned memory, read after the timed region has synced.
-    res_host.copy_(reducer.state[0:2], non_blocking=True)
+    copy_result()
 
   warm, warm_ms, warm_last = warm_up(one_step, args, stream, max_steps=args.warmup + 600)
   torch.cuda.synchronize()
@@ -861,6 +885,9 @@ def main(argv=None):
     if out.get("roofline_effective"):
       out["roofline_effective"].update({"fwd_GBs": None, "fwd_frac": None})
     out["dataflow"] = {"launches_per_sweep": 1, "blocks_fwd": fchunks, "blocks_adj": chunks,
+                       "refine_in_launch": fused_refine,
+                       "refine_to_host": "written by the launch into pinned memory (dg_host_alias)"
+                                         if res_alias is not None else "async copy",
                        "work_items": sweep.op.query_sweep(nsteps)[3],
                        "status": sweep.op.sweep_status()}
     if out["dataflow"]["status"]:

@@ -262,6 +262,16 @@ int dg_lserk4_adj_rec(dg_plan* plan, double* w, const double* jumps, double t0, 
 enum { DG_SWEEP_TERMINAL_STATE = 4 };
 int dg_lserk4_sweep_rec(dg_plan* plan, const double* u0, double* uN, double* w, double* jumps,
                         double t0, double dt, int nsteps, double* eta, int flags, void* stream);
+/* dg_lserk4_sweep_rec followed by the refine decision dg_argmax_ex(eta, batch*K, use_abs = 1,
+ * idx, value, nonfinite_count) -- the single-trajectory adapt iteration of
+ * python/Main_finite_difference.py:336-341 (np.argmax of the indicator) up to the split.
+ * In the dataflow launch the last adjoint block's tiles publish their winners and the last
+ * one to arrive reduces them (no separate reduction kernels); otherwise dg_argmax_ex runs
+ * after the two launch chains.  Same results either way.  eta is required; nsteps >= 1. */
+int dg_lserk4_sweep_refine(dg_plan* plan, const double* u0, double* uN, double* w,
+                           double* jumps, double t0, double dt, int nsteps, double* eta,
+                           int flags, int64_t* idx, double* value, int64_t* nonfinite_count,
+                           void* stream);
 /* out[0] = 1 if dg_lserk4_sweep_rec runs nsteps as one dataflow launch (else the two launch
  * chains), out[1] / out[2] = forward / adjoint steps per block, out[3] = work items. */
 int dg_plan_query_sweep(const dg_plan* plan, int nsteps, int64_t out[4]);
@@ -331,6 +341,11 @@ int dg_argmax_ex(dg_plan* plan, const double* x, int64_t n, int use_abs, int64_t
 /* dst[0:n] = src[0:n] with 16-byte device loads and stores (both 16-byte aligned): the
  * achievable-HBM-bandwidth ceiling of SURVEY 8(d) ("measured with a stream-copy kernel"). */
 int dg_stream_copy(const double* src, double* dst, int64_t n, void* stream);
+
+/* *device = the device address of mapped page-locked host memory `host` (e.g. a pinned
+ * result buffer the refine decision is written to by dg_lserk4_sweep_refine / dg_argmax_ex
+ * with no copy launch); DG_ERR_ARG if it is not such memory. */
+int dg_host_alias(void* host, void** device);
 
 /* out[k] = sum_{r=0}^{rows-1} x[r*n + k], summed in ascending r (bit-reproducible).
  * Ensemble reduction of per-IC indicators (python/Main_width_ref.py:479 mean-over-ICs role). */

@@ -74,8 +74,12 @@ def main():
 
     adj, adj_b = sweep_mean("k_adj")
     fwd, fwd_b = sweep_mean("k_step")
+    dataflow = False
+    sw, sw_b = sweep_mean("k_sweep_rp")
+    if sw:  # the dataflow sweep: one launch per sweep carries both directions' traffic
+      adj, adj_b, fwd, fwd_b, dataflow = sw, sw_b, [], None, True
     tr = {"N": a.N, "K": a.K, "batch": a.batch, "steps_per_launch": a.steps_per_launch,
-          "record": a.record, "source": a.out,
+          "record": a.record, "dataflow": dataflow, "source": a.out,
           "adj_kernel": adj, "adj_bytes_per_launch": adj_b,
           "fwd_kernel": fwd, "fwd_bytes_per_launch": fwd_b,
           "note": "FETCH_SIZE x2 (gfx950 16-B/lane half count) + WRITE_SIZE, KiB->bytes; "

@@ -195,3 +195,100 @@ def test_dataflow_fallbacks(pkg, gpu):
     ref = run_sweep(op, u0, dt, n, False)
     got = run_sweep(op, u0, dt, n, True)  # the fallback inside sweep_rec
     assert_same(got, ref, f"fallback nsteps={n}")
+
+
+@pytest.mark.parametrize("N,K,fsteps,asteps,nsteps", [
+    (4, 1 << 16, 20, 10, 20),   # the bench's shape
+    (4, 9000, 10, 5, 20),
+    (3, 3000, 5, 5, 10),
+    (6, 2048, 20, 10, 40),
+])
+def test_sweep_refine_equals_sweep_then_argmax(pkg, gpu, N, K, fsteps, asteps, nsteps):
+  """dg_lserk4_sweep_refine (the argmax reduced by the dataflow launch's last tiles) gives the
+  index, value and non-finite count of sweep_rec + dg_argmax_ex(|eta|), and the same w, eta;
+  the launch-chain fallback too."""
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  op.tune(rec_tile_width=2, rec_steps_per_launch=asteps, rec_fwd_steps_per_launch=fsteps)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 40 + N, 1)
+  for dataflow in (True, False):
+    op.tune(rec_sweep=1 if dataflow else 0)
+    assert op.query_sweep(nsteps)[0] == dataflow
+    rec, w = op.new_jumps(nsteps), op.new_field()
+    eta = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+    ref = torch.zeros(3, dtype=torch.int64, device=gpu)
+    op.sweep_rec(u0, rec, w, 0.0, dt, nsteps, eta=eta, eta_assign=True, eta_abs=True)
+    op.argmax_ex(eta, ref[0:1], ref[1:2].view(torch.float64), ref[2:3], use_abs=True)
+    eta_ref, w_ref = eta.clone(), w.clone()
+    got = torch.zeros(3, dtype=torch.int64, device=gpu)
+    for rep in range(3):  # repeated launches (the arrival counter grows by the tiles each time)
+      eta.fill_(float("nan"))
+      op.sweep_refine(u0, rec, w, 0.0, dt, nsteps, eta, got[0:1], got[1:2].view(torch.float64),
+                      got[2:3])
+      torch.cuda.synchronize()
+      np.testing.assert_array_equal(host(eta), host(eta_ref))
+      np.testing.assert_array_equal(host(w), host(w_ref))
+      assert host(got)[:2].tolist() == host(ref)[:2].tolist(), (dataflow, rep)
+      assert int(host(got)[0]) == int(np.argmax(np.abs(host(eta_ref))))
+    assert int(host(got)[2]) == 0 and op.sweep_status() == 0
+
+
+def test_sweep_refine_ties_and_nonfinite(pkg, gpu):
+  """numpy.argmax rules in the fused reduction: an exact tie across tiles goes to the lower
+  index; a NaN indicator wins (first NaN) and bumps the non-finite count."""
+  import torch
+  N, K, nsteps = 4, 8192, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh, inflow="zero")
+  op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=20, rec_sweep=1)
+  assert op.query_sweep(nsteps)[0]
+  dt = mesh.cfl_dt()
+  # two identical bumps far apart (translation-invariant interior): their indicator patterns
+  # are equal bit for bit, so the maximum is an exact tie between two tiles
+  x = np.arange(K * (N + 1)) // (N + 1)
+  bump = lambda c: np.exp(-((x - c) / 6.0) ** 2)  # noqa: E731
+  u0h = bump(2000) + bump(6000)
+  u0 = torch.tensor(u0h, dtype=torch.float64, device=gpu)
+  rec, w = op.new_jumps(nsteps), op.new_field()
+  eta = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+  got = torch.zeros(3, dtype=torch.int64, device=gpu)
+  op.sweep_refine(u0, rec, w, 0.0, dt, nsteps, eta, got[0:1], got[1:2].view(torch.float64), got[2:3])
+  torch.cuda.synchronize()
+  e = host(eta)
+  i = int(host(got)[0])
+  assert i == int(np.argmax(e)) and e[i] == e.max()
+  twin = np.flatnonzero(e == e.max())
+  assert len(twin) >= 2 and i == twin[0] and twin[-1] >= 4000, twin  # the tie spans tiles
+  u0[5 * (N + 1) + 2] = float("nan")  # element 5 and its downwind cone turn NaN
+  op.sweep_refine(u0, rec, w, 0.0, dt, nsteps, eta, got[0:1], got[1:2].view(torch.float64), got[2:3])
+  torch.cuda.synchronize()
+  e = host(eta)
+  assert int(host(got)[0]) == int(np.flatnonzero(np.isnan(e))[0])
+  assert np.isnan(host(got[1:2].view(torch.float64))[0]) and int(host(got)[2]) == 1
+
+
+def test_sweep_refine_into_pinned_host_memory(pkg, gpu):
+  """The refine decision written by the launch straight into pinned host memory (its
+  dg_host_alias device address: the bench's path, no copy launch) equals the device one."""
+  import torch
+  mesh = pkg.BaseGalerkin1D(n=4, k=30000)
+  op = pkg.operators.DGAdvection1D(mesh)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 77, 1)
+  rec, w = op.new_jumps(20), op.new_field()
+  eta = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+  dev = torch.zeros(3, dtype=torch.int64, device=gpu)
+  op.sweep_refine(u0, rec, w, 0.0, dt, 20, eta, dev[0:1], dev[1:2].view(torch.float64), dev[2:3])
+  host_buf = torch.full((2,), -7, dtype=torch.int64).pin_memory()
+  alias = pkg.operators.host_alias(host_buf)
+  assert alias is not None
+  assert pkg.operators.host_alias(torch.zeros(2, dtype=torch.int64)) is None  # not pinned
+  nf = torch.zeros(1, dtype=torch.int64, device=gpu)
+  for _ in range(2):
+    host_buf.fill_(-7)
+    op.sweep_refine(u0, rec, w, 0.0, dt, 20, eta, alias, alias + 8, nf)
+    torch.cuda.synchronize()
+    assert host_buf.tolist() == host(dev)[:2].tolist()
+  assert int(nf.item()) == 0
