@@ -480,6 +480,37 @@ def main_config3(args, world, rank, dev):
       "refine_index_ranks": ranks_agree(ref_idx, world, dev, args.backend),
       "K_final": run.K,
   }
+  # Counters from the committed config-3 profile (profiles/r03/collect_c3.sh: FETCH_SIZE /
+  # WRITE_SIZE and SQ fp64 VALU passes of this bench), used when N and K match: HBM traffic
+  # per launch, and the issued fp64 rate = the profile's issued flops per launch / this run's
+  # launch time (every lane of a wave counted: halo lanes included).
+  try:
+    with open(os.path.join(ROOT, "profiles", "r03", "config3", "pmc.json")) as f:
+      prof = json.load(f)
+  except (OSError, ValueError):
+    prof = None
+  if prof and prof.get("N") == N and prof.get("K") == K:
+    uni = "false"  # after its first split the refine loop's mesh is non-uniform
+    pk = {k: v for k, v in prof["kernels"].items() if f", {uni}," in k or k.endswith(f", {uni}>")}
+    ka = next((v for k, v in pk.items() if k.startswith("k_adj_nl")), None)
+    kf = next((v for k, v in pk.items() if k.startswith("k_step_nl") and k.endswith(f", {ms}>")), None)
+    src = prof.get("source")
+    if ka and "hbm_bytes_per_launch" in ka:
+      out["roofline"].update({"traffic": ka["hbm_bytes_per_launch"], "traffic_from_profile": True,
+                              "traffic_source": src})
+    if kf and "hbm_bytes_per_launch" in kf:
+      out["roofline_fwd"].update({"traffic": kf["hbm_bytes_per_launch"],
+                                  "traffic_from_profile": True})
+    if ka and kf and "fp64_flops_issued_per_launch" in ka:
+      at = ka["fp64_flops_issued_per_launch"] / (adj_m * 1e-6) / 1e12
+      ft = kf["fp64_flops_issued_per_launch"] / (fwd_m * 1e-6) / 1e12
+      out["roofline_fp64"] = {
+          "bound": "fp64 vector", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+          "adj_issued": at, "adj_issued_frac": at / FP64_PEAK_TFLOPS,
+          "fwd_issued": ft, "fwd_issued_frac": ft / FP64_PEAK_TFLOPS,
+          "source": src,
+          "what": "fp64 flops issued per launch (PMC: 64 lanes x (2 FMA + ADD + MUL) wave "
+                  "instructions, halo lanes included) / this run's launch time"}
   if rank == 0 and world == 1 and not args.no_cpu_baseline:
     out["cpu_baseline"] = cpu_baseline_config3(N, K, 2)
   if rank == 0:
