@@ -67,6 +67,22 @@ def eo_flops_per_update(Np, adjoint):
   return (5.0 * (6 + 5 * Np + 4 * NE * NO) + 2 * Np + 2) / Np
 
 
+def horner_flops_per_update(Np, adjoint):
+  """fp64 flops per DOF-update of the Horner-form record kernels (pair tiles, dg_rec_tiles.h;
+  k_step_rp / k_adj_rp / k_sweep_rp) for an interior element of a uniform mesh, counted from
+  the code (FMA = 2): per element-step the forward's five levels issue 5 (2 NE NO + Np) FMAs,
+  4 Np multiplies and 21 adds, the adjoint's 5 (2 NE NO + Np) FMAs, 4 Np multiplies and 30
+  adds plus the indicator's Np + 1 FMAs, a multiply and 3 adds -- at Np = 5 211 and 236 flops
+  (126 and 145 instructions), against the stage loop's 265 / 287 (eo_flops_per_update).
+  Checked against PMC: profiles/r03/sq/sq_summary_k_sweep_rp.json issues 10.87 GFLOP per
+  20 + 20-step sweep at K = 2^20, = these counts x the tiles' halo factors (1.25 / 1.11)
+  within 1.5 %."""
+  NE, NO = (Np + 1) // 2, Np // 2
+  if not adjoint:
+    return (21.0 + 14.0 * Np + 20.0 * NE * NO) / Np
+  return (36.0 + 16.0 * Np + 20.0 * NE * NO) / Np
+
+
 def p_flops_per_update(Np):
   """fp64 flops per (order-N) DOF-update of k_adj_p (dg_dwr.hip) for an interior element: per
   element-step the prolongation (even/odd transform + the two blocks), the order-(N+1)
@@ -801,8 +817,12 @@ def main(argv=None):
   idx_ranks = ranks_agree(ref_idx, world, dev, args.backend)
   upl = Np * ktot * float(np.mean(chunks))  # DOF-updates per launch (sweep average)
   fupl = Np * ktot * float(np.mean(fchunks))
-  adj_fpu = p_flops_per_update(Np) if pmode else eo_flops_per_update(Np, True)
-  fwd_fpu = eo_flops_per_update(Np, False)
+  horner = args.record == "jumps" and (pairs or dataflow)  # dg_rec_tiles.h's Horner-form steps
+  if pmode:
+    adj_fpu = p_flops_per_update(Np)
+  else:
+    adj_fpu = horner_flops_per_update(Np, True) if horner else eo_flops_per_update(Np, True)
+  fwd_fpu = horner_flops_per_update(Np, False) if horner else eo_flops_per_update(Np, False)
   adj_tf = adj_fpu * upl / (adj_launch_us * 1e-6) / 1e12
   fwd_tf = fwd_fpu * fupl / (fwd_launch_us * 1e-6) / 1e12
   if dataflow:
@@ -898,7 +918,7 @@ def main(argv=None):
     out["prolong_us"] = float(np.mean(prolong_us))
   if dataflow:
     r = out["roofline"]
-    r["kernel"] = (f"k_sweep_rp<{Np},uniform,1024 elements,fwd {'+'.join(map(str, fchunks))},"
+    r["kernel"] = (f"k_sweep_rp<{Np},uniform,{512 * tw} elements,fwd {'+'.join(map(str, fchunks))},"
                    f"adj {'+'.join(map(str, chunks))},jumps> (ONE dataflow launch per sweep: "
                    f"{nsteps} forward + {nsteps} reverse steps + DWR)")
     r["note"] = ("dataflow sweep (dg_lserk4_sweep_rec): the forward and adjoint blocks' tiles are "
@@ -915,6 +935,19 @@ def main(argv=None):
     out["stream_copy"]["fwd_frac_of_achievable"] = None
     if out.get("roofline_effective"):
       out["roofline_effective"].update({"fwd_GBs": None, "fwd_frac": None})
+    # the PMC-measured issued fp64 flops of the same launch shape (SQ pass of this bench,
+    # profiles/r03/collect_sq_sweep.sh), when N and K match
+    try:
+      with open(os.path.join(ROOT, "profiles", "r03", "sq", "sq_summary_k_sweep_rp.json")) as fh:
+        sq = json.load(fh)
+      if N == 4 and K == (1 << 20) and sweep.batch == 1 and fchunks == [20] and chunks == [10, 10]:
+        fl = sq["fp64_flops_issued_per_launch"]
+        f["pmc_issued_per_launch"] = fl
+        f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
+        f["pmc_issued_over_useful"] = fl / ((fwd_fpu + adj_fpu) * Np * ktot * nsteps)
+        f["pmc_source"] = "profiles/r03/sq/sq_summary_k_sweep_rp.json"
+    except (OSError, ValueError, KeyError):
+      pass
     out["dataflow"] = {"launches_per_sweep": 1, "blocks_fwd": fchunks, "blocks_adj": chunks,
                        "refine_in_launch": fused_refine,
                        "refine_to_host": "written by the launch into pinned memory (dg_host_alias)"
