@@ -66,6 +66,7 @@ SIGNATURES = {
     "dg_lserk4_sweep_refine": (_i32, [_vp, _vp, _vp, _vp, _vp, ctypes.c_double,
                                       ctypes.c_double, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "dg_plan_query_sweep": (_i32, [_vp, _i32, _vp]),
+    "dg_plan_query_sweep_ex": (_i32, [_vp, _i32, _vp]),
     "dg_sweep_status": (_i32, [_vp, ctypes.POINTER(_i32), _vp]),
     "dg_plan_sweep_trace": (_i32, [_vp, _vp]),
     "dg_plan_query_p": (_i32, [_vp, _vp]),

@@ -1069,16 +1069,18 @@ inline int chunk(const dg_plan* p, int left) {
 }
 
 // The dataflow sweep's blocks for `nsteps` steps (dg_sweep.hip): true with the forward /
-// adjoint steps per block when the plan runs it -- pair tiles of 1024 elements in both
-// directions, the record shape's 5-, 10- or 20-step forward and 5- or 10-step adjoint launches
-// as its blocks, nsteps a multiple of both and at most sweep_max_steps() -- else false (the
-// launch-per-block pair runs, with the same results).
-bool sweep_shape(const dg_plan* p, int nsteps, int* msf, int* msa) {
-  const int f = rec_msteps_fwd(p), a = rec_msteps(p);
+// adjoint steps per block when the plan runs it -- pair tiles of one width in both
+// directions (1024 or 512 elements), the record shape's 5-, 10- or 20-step (1024 only)
+// forward and 5- or 10-step adjoint launches as its blocks, nsteps a multiple of both and at
+// most sweep_max_steps() -- else false (the launch-per-block pair runs, same results).
+bool sweep_shape(const dg_plan* p, int nsteps, int* waves, int* msf, int* msa) {
+  const int f = rec_msteps_fwd(p), a = rec_msteps(p), w = p->rec_tile_width;
+  const int nw = 4 * w;
   *msf = f;
   *msa = a;
-  return p->rec_sweep && rec_pairs(p) && rec_fwd_width(p) == 2 && p->rec_tile_width == 2 &&
-         (f == 5 || f == 10 || f == 20) && (a == 5 || a == 10) && nsteps > 0 &&
+  *waves = nw;
+  return p->rec_sweep && rec_pairs(p) && rec_fwd_width(p) == w && (w == 1 || w == 2) &&
+         (f == 5 || f == 10 || (f == 20 && nw == 8)) && (a == 5 || a == 10) && nsteps > 0 &&
          nsteps % f == 0 && nsteps % a == 0 && nsteps <= sweep_max_steps();
 }
 
@@ -1251,6 +1253,7 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     const int k = std::atoi(v);
     if (k == 0 || k == 1) p->rec_sweep = k;
   }
+
   {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
@@ -1709,8 +1712,8 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   const int aflags = flags & (DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS);
   const int64_t field = p->ktot * p->NP;
   const size_t fbytes = sizeof(double) * size_t(field);
-  int msf = 0, msa = 0;
-  if (!sweep_shape(p, nsteps, &msf, &msa)) {
+  int waves = 0, msf = 0, msa = 0;
+  if (!sweep_shape(p, nsteps, &waves, &msf, &msa)) {
     // the launch-per-block pair: forward into uN (or w when it is the terminal weight, or a
     // scratch field), then the adjoint in place on w
     double* fin = uN;
@@ -1727,7 +1730,7 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
     return idx ? dg_argmax_ex(p, eta, p->ktot, 1, idx, value, nonfinite, stream) : DG_OK;
   }
   const int nbF = nsteps / msf, nbA = nsteps / msa;
-  const int64_t items = sweep_items(p, msf, msa, nsteps);
+  const int64_t items = sweep_items(p, waves, msf, msa, nsteps);
   const size_t sync_bytes = (sizeof(uint32_t) * size_t(sweep_sync_words() + items) + 255) & ~size_t(255);
   // fields: forward block outputs U[1..nbF-1] (+ U[nbF] unless the caller keeps u^N), adjoint
   // block outputs W[1..nbA-1] (+ a copy of the caller's terminal weight when one block would
@@ -1735,7 +1738,7 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   const int wcopy = (!term && nbA == 1) ? 1 : 0;
   const int nfields = (nbF - 1) + (uN ? 0 : 1) + (nbA - 1) + wcopy;
   const int nparts = eta ? nbA - 1 : 0;
-  const int64_t am_parts = idx ? sweep_tiles_adj(p, msa) : 0;
+  const int64_t am_parts = idx ? sweep_tiles_adj(p, waves, msa) : 0;
   const size_t bytes = sync_bytes + fbytes * size_t(nfields) +
                        sizeof(double) * size_t(p->ktot) * size_t(nparts) + 16 * size_t(am_parts);
   char* data = nullptr;
@@ -1774,7 +1777,7 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   const int mode = eta ? (kEtaOn | ((aflags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
                           ((aflags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
                        : 0;
-  return sweep_launch_rec(p, msf, msa, b, t0, dt, nsteps, mode, st);
+  return sweep_launch_rec(p, waves, msf, msa, b, t0, dt, nsteps, mode, st);
 }
 }  // namespace
 
@@ -1798,18 +1801,31 @@ int dg_lserk4_sweep_refine(dg_plan* p, const double* u0, double* uN, double* w, 
 
 int dg_plan_query_sweep(const dg_plan* p, int nsteps, int64_t out[4]) {
   if (!p || !out) return fail(DG_ERR_ARG, "null argument");
-  int msf = 0, msa = 0;
-  const bool on = sweep_shape(p, nsteps, &msf, &msa);
+  int waves = 0, msf = 0, msa = 0;
+  const bool on = sweep_shape(p, nsteps, &waves, &msf, &msa);
   out[0] = on ? 1 : 0;
   out[1] = msf;
   out[2] = msa;
-  out[3] = on ? sweep_items(p, msf, msa, nsteps) : 0;
+  out[3] = on ? sweep_items(p, waves, msf, msa, nsteps) : 0;
   return DG_OK;
 }
 
 int dg_plan_sweep_trace(dg_plan* p, uint64_t* trace) {
   if (!p) return fail(DG_ERR_ARG, "null plan");
   p->sweep_trace = trace;
+  return DG_OK;
+}
+
+int dg_plan_query_sweep_ex(const dg_plan* p, int nsteps, int64_t out[6]) {
+  if (!p || !out) return fail(DG_ERR_ARG, "null argument");
+  int waves = 0, msf = 0, msa = 0;
+  const bool on = sweep_shape(p, nsteps, &waves, &msf, &msa);
+  out[0] = on ? 1 : 0;
+  out[1] = msf;
+  out[2] = msa;
+  out[3] = on ? sweep_items(p, waves, msf, msa, nsteps) : 0;
+  out[4] = waves;
+  out[5] = 128 * int64_t(waves);
   return DG_OK;
 }
 

@@ -602,10 +602,10 @@ struct SweepBufs {
   double* am_pv;    // partial winners, one per last-block tile
   int64_t* am_pi;
 };
-int64_t sweep_items(const dg_plan* p, int msf, int msa, int nsteps);
-int64_t sweep_tiles_adj(const dg_plan* p, int msa);
-int sweep_launch_rec(dg_plan* p, int msf, int msa, const SweepBufs& b, double t0, double dt,
-                     int nsteps, int mode, hipStream_t st);
+int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps);
+int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa);
+int sweep_launch_rec(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,
+                     double dt, int nsteps, int mode, hipStream_t st);
 int sweep_sync_words();
 int sweep_max_steps();
 int sweep_err_word();

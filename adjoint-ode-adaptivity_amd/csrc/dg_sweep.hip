@@ -47,9 +47,6 @@ constexpr int kSweepMaxBlocks = 8;   // blocks per direction (kSweepMaxSteps / 5
 // counter of the fused refine decision, then one flag per item
 constexpr int kSyncHead = 0, kSyncErr = 2, kSyncArrive = 4, kSyncFlags = 16;
 constexpr int kSweepSpinLimit = 1 << 20;
-#ifndef DG_SWEEP_WAVES
-#define DG_SWEEP_WAVES 5
-#endif
 
 template <int NP, int MSF> struct SweepArgs {
   RpOp<NP> c;
@@ -99,8 +96,9 @@ __device__ __forceinline__ void sweep_wait(const uint32_t* flags, int nd, uint32
   }
 }
 
-// Winner of (v, i) over the 512-lane workgroup under am_better; valid in thread 0.  sv / si:
-// 8 LDS slots of the caller's own (not aliased with a tile image another wave may read).
+// Winner of (v, i) over the NW-wave workgroup under am_better; valid in thread 0.  sv / si:
+// NW LDS slots of the caller's own (not aliased with a tile image another wave may read).
+template <int NW>
 __device__ __forceinline__ void wg_argmax(double& v, int64_t& i, double* sv, int64_t* si) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -118,7 +116,7 @@ __device__ __forceinline__ void wg_argmax(double& v, int64_t& i, double* sv, int
   }
   __syncthreads();
   if (threadIdx.x == 0)
-    for (int k = 1; k < 8; ++k)
+    for (int k = 1; k < NW; ++k)
       if (am_better(sv[k], si[k], v, i)) {
         v = sv[k];
         i = si[k];
@@ -134,17 +132,16 @@ __device__ __forceinline__ uint64_t ld8_agent(const void* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int NP, bool UNI, int MSF, int MSA>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WAVES))) void k_sweep_rp(
-    SweepArgs<NP, MSF> a) {
-  constexpr int NW = 8, E = 2;
+template <int NP, bool UNI, int NW, int MSF, int MSA>
+__global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
+  constexpr int E = 2;
   using G = RpGeo<NP, NW, E>;
   constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
   constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MSF * 6 + 1];
   __shared__ uint32_t s_item, s_epoch, s_last;
-  __shared__ double s_av[8];
-  __shared__ int64_t s_ai[8];
+  __shared__ double s_av[NW];
+  __shared__ int64_t s_ai[NW];
   uint32_t* sync = a.sync;
   uint32_t* flags = sync + kSyncFlags;
   const int tid = threadIdx.x;
@@ -208,7 +205,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
       const int64_t e0 = int64_t(j) * TEF - HF;
       using SA = SweepArgs<NP, MSF>;
       const double* kb = reinterpret_cast<const double*>(
-                             kernarg_tail<decltype(&k_sweep_rp<NP, UNI, MSF, MSA>), SA>() +
+                             kernarg_tail<decltype(&k_sweep_rp<NP, UNI, NW, MSF, MSA>), SA>() +
                              offsetof(SA, bnd)) + blk * (MSF * 6 + 1);
       const int64_t n0 = int64_t(blk) * MSF;
       const bool jend = blk == a.nbF - 1;
@@ -239,7 +236,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
         rp_adj_tile<NP, UNI, NW, E, MSA, false, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
                                                       a.scale, a.c, n0);
       if (es.argmax) {  // the tile's winner, a hand-off to the last arriving tile
-        wg_argmax(es.bv, es.bi, s_av, s_ai);
+        wg_argmax<NW>(es.bv, es.bi, s_av, s_ai);
         if (tid == 0) {
           st8_agent(a.am_pv + j, __builtin_bit_cast(uint64_t, es.bv));
           st8_agent(a.am_pi + j, uint64_t(es.bi));
@@ -265,7 +262,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         double v = -INFINITY;
         int64_t i = INT64_MAX;
-        for (int q = tid; q < nTA; q += 512) {
+        for (int q = tid; q < nTA; q += 64 * NW) {
           const double pv = __builtin_bit_cast(double, ld8_agent(a.am_pv + q));
           const int64_t pi = int64_t(ld8_agent(a.am_pi + q));
           if (am_better(pv, pi, v, i)) {
@@ -273,7 +270,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
             i = pi;
           }
         }
-        wg_argmax(v, i, s_av, s_ai);
+        wg_argmax<NW>(v, i, s_av, s_ai);
         if (tid == 0) {
           a.am_idx[0] = i;
           if (a.am_val) a.am_val[0] = v;
@@ -295,7 +292,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(DG_SWEEP_WA
 
 static_assert(kSweepMaxBlocks + 1 == sizeof(SweepBufs::U) / sizeof(double*), "SweepBufs");
 
-template <int NP, bool UNI, int MSF, int MSA>
+template <int NP, bool UNI, int NW, int MSF, int MSA>
 int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int nsteps,
                  int mode, hipStream_t st) {
   SweepArgs<NP, MSF> a;
@@ -323,59 +320,75 @@ int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int 
   a.am_pi = b.am_pi;
   a.nbF = nbF;
   a.nbA = nbA;
-  using G = RpGeo<NP, 8, 2>;
+  using G = RpGeo<NP, NW, 2>;
   a.nTF = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSF>::F));
   a.nTA = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSA>::A));
   a.nsteps = nsteps;
   a.mode = mode;
   a.spin_limit = kSweepSpinLimit;
   const int64_t items = int64_t(nbF) * a.nTF + int64_t(nbA) * a.nTA;
-  hipLaunchKernelGGL((k_sweep_rp<NP, UNI, MSF, MSA>), dim3(unsigned(items)), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((k_sweep_rp<NP, UNI, NW, MSF, MSA>), dim3(unsigned(items)), dim3(64 * NW), 0,
+                     st, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-template <int NP, bool UNI>
+template <int NP, bool UNI, int NW>
 int sweep_shape_launch(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0,
                        double dt, int nsteps, int mode, hipStream_t st) {
   if (msa == 10) {
-    if (msf == 20) return sweep_launch<NP, UNI, 20, 10>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 10) return sweep_launch<NP, UNI, 10, 10>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 5) return sweep_launch<NP, UNI, 5, 10>(p, b, t0, dt, nsteps, mode, st);
+    if constexpr (NW == 8)
+      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 10>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 10>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 10>(p, b, t0, dt, nsteps, mode, st);
   } else if (msa == 5) {
-    if (msf == 20) return sweep_launch<NP, UNI, 20, 5>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 10) return sweep_launch<NP, UNI, 10, 5>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 5) return sweep_launch<NP, UNI, 5, 5>(p, b, t0, dt, nsteps, mode, st);
+    if constexpr (NW == 8)
+      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 5>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 5>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 5>(p, b, t0, dt, nsteps, mode, st);
   }
-  return fail(DG_ERR_ARG, "dataflow sweep: unsupported steps per block");
+  return fail(DG_ERR_ARG, "dataflow sweep: unsupported steps per block for this tile width");
 }
 
+template <int NP, int NW>
+int sweep_uni(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0, double dt,
+              int nsteps, int mode, hipStream_t st) {
+  return p->uniform ? sweep_shape_launch<NP, true, NW>(p, msf, msa, b, t0, dt, nsteps, mode, st)
+                    : sweep_shape_launch<NP, false, NW>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+}
+
+// Tiles of 128 * waves elements on workgroups of `waves` waves: 8 (1024 elements, the
+// default) or 4 (512: tile width 1).  Workgroups of 5, 6 and 10 waves (which fill the 20 wave
+// slots per CU the 88-VGPR bodies leave, where 8-wave groups use 16) measured 17-27 % slower
+// at N = 4, K = 2^20 (profiles/r03/waves2/: more items and their per-item latency, or a
+// barrier over 10 waves) and were dropped.
 template <int NP>
-int sweep_np(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0, double dt,
-             int nsteps, int mode, hipStream_t st) {
-  return p->uniform ? sweep_shape_launch<NP, true>(p, msf, msa, b, t0, dt, nsteps, mode, st)
-                    : sweep_shape_launch<NP, false>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+int sweep_np(dg_plan* p, int waves, int msf, int msa, const dgk::SweepBufs& b, double t0,
+             double dt, int nsteps, int mode, hipStream_t st) {
+  if (waves == 8) return sweep_uni<NP, 8>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+  if (waves == 4) return sweep_uni<NP, 4>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+  return fail(DG_ERR_ARG, "dataflow sweep: workgroups of 4 or 8 waves");
 }
 
 }  // namespace
 
 namespace dgk {
 
-int64_t sweep_items(const dg_plan* p, int msf, int msa, int nsteps) {
-  constexpr int T = 1024;
+int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps) {
+  const int T = 128 * waves;
   const int64_t nTF = grid_for(p->ktot, T - 2 * ((msf * 5 + 2) & ~1));
   const int64_t nTA = grid_for(p->ktot, T - 2 * ((msa * 5 + 1) & ~1));
   return int64_t(nsteps / msf) * nTF + int64_t(nsteps / msa) * nTA;
 }
 
-int64_t sweep_tiles_adj(const dg_plan* p, int msa) {
-  return grid_for(p->ktot, 1024 - 2 * ((msa * 5 + 1) & ~1));
+int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa) {
+  return grid_for(p->ktot, 128 * waves - 2 * ((msa * 5 + 1) & ~1));
 }
 
-int sweep_launch_rec(dg_plan* p, int msf, int msa, const SweepBufs& b, double t0, double dt,
-                     int nsteps, int mode, hipStream_t st) {
+int sweep_launch_rec(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,
+                     double dt, int nsteps, int mode, hipStream_t st) {
   int rc = DG_OK;
-  DG_DISPATCH_NP(p->NP, rc = sweep_np<NP>(p, msf, msa, b, t0, dt, nsteps, mode, st));
+  DG_DISPATCH_NP(p->NP, rc = sweep_np<NP>(p, waves, msf, msa, b, t0, dt, nsteps, mode, st));
   return rc;
 }
 

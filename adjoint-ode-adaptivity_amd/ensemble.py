@@ -245,6 +245,22 @@ class DeviceReducer:
   def argmax(self, x):
     return self.op.argmax_ex(x.contiguous(), self.idx, self.value, self.nonfinite, use_abs=True)
 
+  def argmax_value(self, x):
+    """(index, |x[index]|) of argmax |x| as (1,) device tensors, state untouched."""
+    i = torch.empty(1, dtype=torch.int64, device=self.op.device)
+    v = torch.empty(1, dtype=torch.float64, device=self.op.device)
+    self.op.argmax_ex(x.contiguous(), i, v, None, use_abs=True)
+    return i, v
+
+  def finish(self, values, indices):
+    """The refine decision from per-rank candidates (values (W,) float64, indices (W,) int64,
+    rank order): the argmax of the values under numpy's order (ties to the lowest rank, which
+    owns the lowest indices) into the state, then its index."""
+    w = torch.empty(1, dtype=torch.int64, device=self.op.device)
+    self.op.argmax_ex(values.contiguous(), w, self.value, self.nonfinite, use_abs=False)
+    torch.index_select(indices.contiguous(), 0, w, out=self.idx)
+    return self.idx
+
 
 def _exchange(coll, send, group, n_out=None):
   """out = coll(out, send) over the process group.  RCCL ("nccl") moves device tensors over
@@ -286,6 +302,43 @@ def gather_indicator(partial, n_total, reducer, group=None):
   # dividing by 1 is exact (bit-identical shortcut)
   mean = total / float(n_total) if n_total != 1 else total
   return mean, reducer.argmax(mean)
+
+
+def refine_decision(partial, n_total, reducer, group=None):
+  """The refine decision of ``gather_indicator`` (argmax of the mean indicator's magnitude,
+  python/Main_width_ref.py:491) without materialising the mean on every rank: after the
+  rank-ordered all-to-all each rank takes the argmax of its summed slice's mean, and the W
+  (value, index) candidates are all-gathered -- 16 B per rank instead of the (W-1)/W K doubles
+  of gathering the summed slices.  The winner is the argmax over the candidates under
+  numpy's order: a tie goes to the lowest rank, which owns the lowest indices, and a NaN
+  anywhere wins as it would in the full vector, so index and value are those of
+  ``gather_indicator`` bit for bit (the slices hold the same doubles).  One rank: exactly
+  ``gather_indicator``.  Returns the index tensor (the reducer's state holds index, value and
+  the non-finite count)."""
+  if dist.is_available() and dist.is_initialized():
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+  else:
+    world, rank = 1, 0
+  if world == 1:
+    return gather_indicator(partial, n_total, reducer, group)[1]
+  K = partial.numel()
+  chunk = -(-K // world)
+  send = partial.new_zeros(world * chunk)
+  send[:K] = partial.reshape(-1)
+  recv = _exchange(dist.all_to_all_single, send, group)
+  mine = reducer.sum_rows(recv.view(world, chunk))  # rank order
+  lo = rank * chunk
+  n = max(0, min(chunk, K - lo))
+  if n > 0:
+    sl = mine[:n]
+    mean = sl / float(n_total) if n_total != 1 else sl
+    i, v = reducer.argmax_value(mean)
+    cand = torch.cat([v.reshape(1).view(torch.int64), i.reshape(1) + lo])
+  else:  # a rank past the end of K: the weakest candidate
+    cand = torch.tensor([np.array([-np.inf]).view(np.int64)[0], np.iinfo(np.int64).max],
+                        dtype=torch.int64, device=partial.device)
+  allc = _exchange(dist.all_gather_into_tensor, cand.contiguous(), group, 2 * world).view(world, 2)
+  return reducer.finish(allc[:, 0].contiguous().view(torch.float64), allc[:, 1].contiguous())
 
 
 _KEEP = {}

@@ -358,12 +358,15 @@ class DGAdvection1D:
     _lib.check(rc, "dg_lserk4_sweep_refine")
     return idx
 
-  def query_sweep(self, nsteps):
+  def query_sweep(self, nsteps, tile=False):
     """(dataflow, forward steps per block, adjoint steps per block, work items) of
-    ``sweep_rec`` for an ``nsteps`` sweep; dataflow False: the two launch chains run."""
-    q = (ctypes.c_int64 * 4)()
-    _lib.check(self._lib.dg_plan_query_sweep(self._plan, int(nsteps), q), "dg_plan_query_sweep")
-    return bool(q[0]), int(q[1]), int(q[2]), int(q[3])
+    ``sweep_rec`` for an ``nsteps`` sweep; dataflow False: the two launch chains run.
+    ``tile``: also (workgroup waves, elements per tile)."""
+    q = (ctypes.c_int64 * 6)()
+    _lib.check(self._lib.dg_plan_query_sweep_ex(self._plan, int(nsteps), q),
+               "dg_plan_query_sweep_ex")
+    out = (bool(q[0]), int(q[1]), int(q[2]), int(q[3]))
+    return out + (int(q[4]), int(q[5])) if tile else out
 
   def sweep_trace(self, trace):
     """Profiling: record per work item of every later dataflow sweep {taken, producers done,

@@ -649,7 +649,7 @@ def main(argv=None):
       if ev:
         ev[2].record(stream)
       partial = sweep.reduce()
-      ens.gather_indicator(partial, n_total, reducer)
+      ens.refine_decision(partial, n_total, reducer)
       if args.gather_ics:
         ens.gather_per_ic(sweep.per_ic(), n_total)
       copy_result()
@@ -665,7 +665,7 @@ def main(argv=None):
     if ev:
       ev[2].record(stream)
     partial = sweep.reduce()
-    ens.gather_indicator(partial, n_total, reducer)
+    ens.refine_decision(partial, n_total, reducer)
     if args.gather_ics:
       ens.gather_per_ic(sweep.per_ic(), n_total)
     # The refine index (the mesh split's input) and the indicator there go to the host in
@@ -756,9 +756,11 @@ def main(argv=None):
   # Issued vs useful lanes: each tile recomputes a halo of H elements per side (the
   # dependency cone of its fused steps) and writes T - 2H, weighted by steps.
   if pairs:
-    # pair tiles: 512 elements per tile width; halos rounded up to even (aligned record
-    # pairs, dg_rec.hip RpHalo), the forward's one wider for the final jumps
-    T_of = lambda m, fwd: 512 * tw  # noqa: E731
+    # pair tiles: 512 elements per tile width (the dataflow launch: 128 per workgroup wave);
+    # halos rounded up to even (aligned record pairs, dg_rec.hip RpHalo), the forward's one
+    # wider for the final jumps
+    T_pair = sweep.op.query_sweep(nsteps, tile=True)[5] if dataflow else 512 * tw
+    T_of = lambda m, fwd: T_pair  # noqa: E731
     h_fwd = lambda m: (5 * m + 2) & ~1  # noqa: E731
     h_adj = lambda m: (5 * m + 1) & ~1  # noqa: E731
   elif args.record == "jumps":
@@ -918,7 +920,7 @@ def main(argv=None):
     out["prolong_us"] = float(np.mean(prolong_us))
   if dataflow:
     r = out["roofline"]
-    r["kernel"] = (f"k_sweep_rp<{Np},uniform,{512 * tw} elements,fwd {'+'.join(map(str, fchunks))},"
+    r["kernel"] = (f"k_sweep_rp<{Np},uniform,{T_pair} elements,fwd {'+'.join(map(str, fchunks))},"
                    f"adj {'+'.join(map(str, chunks))},jumps> (ONE dataflow launch per sweep: "
                    f"{nsteps} forward + {nsteps} reverse steps + DWR)")
     r["note"] = ("dataflow sweep (dg_lserk4_sweep_rec): the forward and adjoint blocks' tiles are "
@@ -940,7 +942,8 @@ def main(argv=None):
     try:
       with open(os.path.join(ROOT, "profiles", "r03", "sq", "sq_summary_k_sweep_rp.json")) as fh:
         sq = json.load(fh)
-      if N == 4 and K == (1 << 20) and sweep.batch == 1 and fchunks == [20] and chunks == [10, 10]:
+      if (N == 4 and K == (1 << 20) and sweep.batch == 1 and fchunks == [20]
+          and chunks == [10, 10] and T_pair == 1024):
         fl = sq["fp64_flops_issued_per_launch"]
         f["pmc_issued_per_launch"] = fl
         f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS

@@ -275,6 +275,8 @@ int dg_lserk4_sweep_refine(dg_plan* plan, const double* u0, double* uN, double* 
 /* out[0] = 1 if dg_lserk4_sweep_rec runs nsteps as one dataflow launch (else the two launch
  * chains), out[1] / out[2] = forward / adjoint steps per block, out[3] = work items. */
 int dg_plan_query_sweep(const dg_plan* plan, int nsteps, int64_t out[4]);
+/* dg_plan_query_sweep plus out[4] = workgroup waves, out[5] = elements per tile. */
+int dg_plan_query_sweep_ex(const dg_plan* plan, int nsteps, int64_t out[6]);
 /* Synchronises `stream`; *status = 0, or 1 if a dataflow sweep since the last call gave up
  * waiting for a producer (a bug: its outputs are garbage; the launch still ended). */
 int dg_sweep_status(dg_plan* plan, int* status, void* stream);

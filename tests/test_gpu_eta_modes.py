@@ -133,3 +133,34 @@ def test_stream_copy_rejects_misaligned(pkg, gpu):
   dst = torch.zeros(101, dtype=torch.float64, device=gpu)
   with pytest.raises(pkg._lib.DGLibraryError, match="aligned"):
     pkg.operators.stream_copy(src[1:], dst[1:])
+
+
+@pytest.mark.parametrize("kind", ["rand", "tie", "nan"])
+def test_device_reducer_candidates_pick_the_full_argmax(pkg, gpu, kind):
+  """DeviceReducer.argmax_value / finish, the device half of ensemble.refine_decision: the
+  per-slice (value, global index) candidates of W ranks, reduced in rank order, give the
+  index and value of numpy's argmax of |x| over the whole vector (the collectives around
+  them are covered on CPU by tests/test_dist_gloo.py)."""
+  import torch
+  K, W = 10007, 4
+  mesh = pkg.BaseGalerkin1D(n=2, k=K)
+  red = pkg.ensemble.DeviceReducer(pkg.operators.DGAdvection1D(mesh))
+  rng = np.random.default_rng(11)
+  x = np.abs(rng.standard_normal(K))
+  if kind == "tie":
+    x[[9000, 2600, 2500]] = 7.0  # equal maxima in slices 3, 1, 0: the lowest index wins
+  elif kind == "nan":
+    x[[100, 8000]] = [1e6, np.nan]
+  chunk = -(-K // W)
+  vals, idxs = [], []
+  for r in range(W):
+    sl = torch.tensor(x[r * chunk:(r + 1) * chunk], device=gpu)
+    i, v = red.argmax_value(sl)
+    vals.append(v)
+    idxs.append(i + r * chunk)
+  out = red.finish(torch.cat(vals), torch.cat(idxs))
+  torch.cuda.synchronize()
+  want = oadj.argmax(x, use_abs=True)
+  assert int(out[0]) == int(red.idx[0]) == want
+  np.testing.assert_array_equal(host(red.value), np.abs(x[want:want + 1]))
+  assert int(red.nonfinite[0]) == (1 if kind == "nan" else 0)

@@ -65,21 +65,24 @@ def assert_same(a, b, what):
     np.testing.assert_array_equal(x, y, err_msg=f"{what}: {name}")
 
 
-@pytest.mark.parametrize("N,K,batch,fsteps,nsteps,inflow,refined", [
-    (4, 5000, 1, 20, 20, "a", False),      # the bench's shape: forward 20, adjoint 10 + 10
-    (4, 5000, 1, 10, 20, "a", False),      # forward 10 + 10
-    (4, 3000, 3, 20, 40, "a2", False),    # trajectory edges inside tiles, 2 + 4 blocks
-    (4, 2500, 2, 10, 30, "a", False),      # 3 + 3 blocks
-    (1, 4000, 1, 20, 20, "a", False),
-    (2, 1500, 2, 10, 10, "a", False),      # one block each way
-    (3, 2000, 1, 20, 20, "zero", False),
-    (5, 2000, 2, 20, 20, "a", False),
-    (6, 1200, 1, 10, 20, "a", False),
-    (7, 1100, 1, 20, 20, "a", False),
-    (4, 3000, 2, 20, 20, "a", True),       # refined (non-uniform metric)
-    (4, 700, 1, 20, 20, "a", False),       # fewer elements than one tile's output
+@pytest.mark.parametrize("N,K,batch,fsteps,nsteps,inflow,refined,width", [
+    (4, 5000, 1, 20, 20, "a", False, 2),      # the bench's shape: forward 20, adjoint 10 + 10
+    (4, 5000, 1, 10, 20, "a", False, 2),      # forward 10 + 10
+    (4, 3000, 3, 20, 40, "a2", False, 2),     # trajectory edges inside tiles, 2 + 4 blocks
+    (4, 2500, 2, 10, 30, "a", False, 2),      # 3 + 3 blocks
+    (1, 4000, 1, 20, 20, "a", False, 2),
+    (2, 1500, 2, 10, 10, "a", False, 2),      # one block each way
+    (3, 2000, 1, 20, 20, "zero", False, 2),
+    (5, 2000, 2, 20, 20, "a", False, 2),
+    (6, 1200, 1, 10, 20, "a", False, 2),
+    (7, 1100, 1, 20, 20, "a", False, 2),
+    (4, 3000, 2, 20, 20, "a", True, 2),       # refined (non-uniform metric)
+    (4, 700, 1, 20, 20, "a", False, 2),       # fewer elements than one tile's output
+    (8, 3000, 2, 10, 20, "a", False, 1),      # Np = 9 on 512-element tiles (4-wave workgroups)
+    (4, 2000, 1, 5, 20, "a2", True, 1),       # 512-element tiles, 4 + 2 blocks, refined
 ])
-def test_dataflow_equals_launch_chains(pkg, gpu, N, K, batch, fsteps, nsteps, inflow, refined):
+def test_dataflow_equals_launch_chains(pkg, gpu, N, K, batch, fsteps, nsteps, inflow, refined,
+                                       width):
   v_x = np.linspace(0.0, 1.0, K + 1)
   if refined:
     for k in (3, 900, 901, K - 1):
@@ -87,7 +90,7 @@ def test_dataflow_equals_launch_chains(pkg, gpu, N, K, batch, fsteps, nsteps, in
   mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
   op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
   assert op.uniform != refined
-  op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=fsteps)
+  op.tune(rec_tile_width=width, rec_steps_per_launch=10, rec_fwd_steps_per_launch=fsteps)
   on, msf, msa, items = op.query_sweep(nsteps)
   assert on and (msf, msa) == (fsteps, 10) and items > 0
   dt = mesh.cfl_dt()
@@ -187,7 +190,11 @@ def test_dataflow_fallbacks(pkg, gpu):
   op.tune(rec_sweep=0)
   assert not op.query_sweep(20)[0]
   op.tune(rec_sweep=1, rec_tile_width=1, rec_steps_per_launch=10)
-  assert not op.query_sweep(20)[0]
+  assert op.query_sweep(20)[0]  # 512-element tiles, 10-step blocks
+  op.tune(rec_fwd_steps_per_launch=20)
+  assert op.query_sweep(20)[:3] == (True, 10, 10)  # 512-element tiles cap the blocks at 10
+  op.tune(rec_tile_width=2, rec_fwd_tile_width=1)
+  assert not op.query_sweep(20)[0]  # one tile width for both directions
   op.tune(rec_tile_width=2, rec_steps_per_launch=10, rec_fwd_steps_per_launch=20)
   dt = mesh.cfl_dt()
   u0 = noisy_sine(op, 4, 1)
@@ -197,20 +204,21 @@ def test_dataflow_fallbacks(pkg, gpu):
     assert_same(got, ref, f"fallback nsteps={n}")
 
 
-@pytest.mark.parametrize("N,K,fsteps,asteps,nsteps", [
-    (4, 1 << 16, 20, 10, 20),   # the bench's shape
-    (4, 9000, 10, 5, 20),
-    (3, 3000, 5, 5, 10),
-    (6, 2048, 20, 10, 40),
+@pytest.mark.parametrize("N,K,fsteps,asteps,nsteps,width", [
+    (4, 1 << 16, 20, 10, 20, 2),   # the bench's shape
+    (4, 9000, 10, 5, 20, 2),
+    (3, 3000, 5, 5, 10, 2),
+    (6, 2048, 20, 10, 40, 2),
+    (5, 20000, 10, 10, 20, 1),     # 512-element tiles: the reduction over 4 waves
 ])
-def test_sweep_refine_equals_sweep_then_argmax(pkg, gpu, N, K, fsteps, asteps, nsteps):
+def test_sweep_refine_equals_sweep_then_argmax(pkg, gpu, N, K, fsteps, asteps, nsteps, width):
   """dg_lserk4_sweep_refine (the argmax reduced by the dataflow launch's last tiles) gives the
   index, value and non-finite count of sweep_rec + dg_argmax_ex(|eta|), and the same w, eta;
   the launch-chain fallback too."""
   import torch
   mesh = pkg.BaseGalerkin1D(n=N, k=K)
   op = pkg.operators.DGAdvection1D(mesh)
-  op.tune(rec_tile_width=2, rec_steps_per_launch=asteps, rec_fwd_steps_per_launch=fsteps)
+  op.tune(rec_tile_width=width, rec_steps_per_launch=asteps, rec_fwd_steps_per_launch=fsteps)
   dt = mesh.cfl_dt()
   u0 = noisy_sine(op, 40 + N, 1)
   for dataflow in (True, False):
