@@ -1291,6 +1291,7 @@ int dg_plan_destroy(dg_plan* p) {
   if (p->d_pv) (void)hipFree(p->d_pv);
   if (p->d_pi) (void)hipFree(p->d_pi);
   if (p->d_sweep) (void)hipFree(p->d_sweep);
+  if (p->d_nl_list) (void)hipFree(p->d_nl_list);
   delete p;
   return DG_OK;
 }

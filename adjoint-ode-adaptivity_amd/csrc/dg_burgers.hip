@@ -391,10 +391,18 @@ __global__ __launch_bounds__(kBlock * kNLAdjW, kNLAdjMinWaves) void k_adj_nl(con
                                                    double* __restrict__ eta,
                                                    const double* __restrict__ scale,
                                                    const uint16_t* __restrict__ codes,
+                                                   int32_t* __restrict__ list,
+                                                   int32_t* __restrict__ count,
                                                    NLAdjArgs<NP> args);
 
-template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN, bool EDGE>
-__device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t tile,
+// One tile of the reverse step: the T elements from e0 on, of which lanes [H, H + nout)
+// are outputs.  H is the dependency cone: 20 elements (10 stages of 2) in general, 10 (1 per
+// stage) for a FAST tile, valid only when no cell of the tile is troubled in any stage of
+// the step; a FAST tile finds that out from the decision record right after its loads and
+// returns false, before any store, when it does not hold (the caller then recomputes its
+// outputs on the wide cone).
+template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN, bool EDGE, int H, bool FAST>
+__device__ __forceinline__ bool nl_adj_tile(double* __restrict__ lds, int64_t e0, int nout,
                                             const double* __restrict__ win,
                                             double* __restrict__ wout,
                                             const double* __restrict__ snap,
@@ -403,14 +411,11 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
                                             const uint16_t* __restrict__ codes,
                                             const NLAdjArgs<NP>& args) {
   constexpr int W = kNLAdjW, T = kBlock * W, NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
-  // forward recompute and reverse sweep each widen the cone by one stage-cone per stage
-  constexpr int H = 10 * cone_per_stage<LIM>();
-  constexpr int TE = T - 2 * H;
-  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  static_assert(!FAST || KNOWN, "a FAST tile needs the decision record");
+  static_assert(H > 0 && 2 * H < T, "tile geometry");
   constexpr int CB = NLGeo<NP, W>::kLds;  // lds[CB+s]: stage inflow flux; CB+5: residual's; CB+6: 0
   constexpr int CL = NLGeo<NP, W>::CL, CR = NLGeo<NP, W>::CR;
   const int lane = threadIdx.x;
-  const int64_t e0 = tile * TE - H;
   const int64_t nd = args.ktot * NP;
 
   // The decision record is loaded first, with the tiles, so its latency hides behind theirs.
@@ -420,7 +425,8 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     kcode = (e >= 0 && e < args.ktot) ? int(codes[e]) : 0;
   }
   // the element's metric likewise
-  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  E.valid = E.valid && lane < H + nout;
   double sc = args.sc;
   if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
   TileRegs<NP, W> pu, pw;
@@ -464,6 +470,9 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
   //    others the limiter and its exchange are skipped, here and in the reverse pass.
   int wg = 0;
   if constexpr (KNOWN) wg = wg_or;  // the load phase's barriers ordered its init and ORs
+  if constexpr (FAST) {
+    if (wg != 0) return false;  // (workgroup-uniform) some cell is troubled: the wide cone
+  }
   // The stage inputs u_s feed the Burgers flux Jacobian of the reverse pass.  Registers
   // hold u_2..u_4; u_1 goes to a lane-private LDS slot and u_0 = u^n is re-read from the
   // snapshot (L2-resident) at the end: 20 VGPRs fewer at the peak (5 waves per SIMD
@@ -690,6 +699,7 @@ __device__ __forceinline__ void nl_adj_tile(double* __restrict__ lds, int64_t ti
     }
     if constexpr (NE > NO) o[NO] = we[NO];
   }
+  return true;
 }
 
 template <int NP, bool BURG, bool LIM, bool UNI, bool KNOWN>
@@ -699,19 +709,65 @@ __global__ __launch_bounds__(kBlock * kNLAdjW, kNLAdjMinWaves) void k_adj_nl(con
                                                    double* __restrict__ eta,
                                                    const double* __restrict__ scale,
                                                    const uint16_t* __restrict__ codes,
+                                                   int32_t* __restrict__ list,
+                                                   int32_t* __restrict__ count,
                                                    NLAdjArgs<NP> args) {
-  constexpr int T = kBlock * kNLAdjW, H = 10 * cone_per_stage<LIM>();
+  // forward recompute and reverse sweep each widen the cone by one stage-cone per stage
+  constexpr int T = kBlock * kNLAdjW, HW = 10 * cone_per_stage<LIM>();
+  // With the decision record, tiles are laid out for the narrow cone (1 element per stage:
+  // no troubled cell, the case of almost every tile); a tile with a troubled cell in its
+  // range recomputes its outputs as two halves on the wide cone.  The results are the same
+  // numbers either way: each output's value depends only on its cone.
+  constexpr int H = KNOWN ? 10 : HW, TE = T - 2 * H, TH = TE / 2;
+  static_assert(TE % 2 == 0 && TE > 0 && (!KNOWN || TH + 2 * HW <= T), "tile geometry");
   // boundary constants (8 slots), then the lane-private stage-1 input (Burgers only)
   __shared__ __attribute__((aligned(16)))
   double lds[NLGeo<NP, kNLAdjW>::kLds + 8 + (BURG ? T * NP : 0)];
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
-  const int64_t e0 = tile * (T - 2 * H) - H;
+  const int64_t e0 = tile * TE - H;
+  bool done;
   if (edge_tile(e0, T, args.ktot, args.K))
-    nl_adj_tile<NP, BURG, LIM, UNI, KNOWN, true>(lds, tile, win, wout, snap, eta, scale, codes,
-                                                 args);
+    done = nl_adj_tile<NP, BURG, LIM, UNI, KNOWN, true, H, KNOWN>(lds, e0, TE, win, wout, snap,
+                                                                   eta, scale, codes, args);
   else
-    nl_adj_tile<NP, BURG, LIM, UNI, KNOWN, false>(lds, tile, win, wout, snap, eta, scale, codes,
-                                                  args);
+    done = nl_adj_tile<NP, BURG, LIM, UNI, KNOWN, false, H, KNOWN>(lds, e0, TE, win, wout, snap,
+                                                                    eta, scale, codes, args);
+  if constexpr (KNOWN) {
+    // a troubled tile goes on the list for k_adj_nl_wide (this step's count, zeroed per sweep)
+    if (!done && threadIdx.x == 0) list[atomicAdd(count, 1)] = int32_t(tile);
+  }
+}
+
+// The tiles k_adj_nl listed as troubled, each recomputed as two half tiles on the wide cone
+// (20 elements of halo, 118 outputs each).  A separate launch so that neither kernel carries
+// the other's registers (one kernel with both bodies spilled 69 VGPRs).  Grid-stride over
+// the (tile, half) items -- almost always none.  Each step of a sweep has its own count
+// (nl_adj zeroes them once per sweep), so nothing is reset here: an exit counter for a
+// reset, one same-address atomic per workgroup, cost ~10 us per launch.  Same parameter list
+// as k_adj_nl: the edge tiles read their constants at k_adj_nl's kernarg offsets.  4 waves
+// per SIMD: at 5 the item loop's live kernel arguments spilled 20 VGPRs.
+template <int NP, bool BURG, bool LIM, bool UNI>
+__global__ __launch_bounds__(kBlock * kNLAdjW, 4) void k_adj_nl_wide(
+    const double* __restrict__ win, double* __restrict__ wout, const double* __restrict__ snap,
+    double* __restrict__ eta, const double* __restrict__ scale,
+    const uint16_t* __restrict__ codes, int32_t* __restrict__ list, int32_t* __restrict__ count,
+    NLAdjArgs<NP> args) {
+  constexpr int T = kBlock * kNLAdjW, HW = 10 * cone_per_stage<LIM>(), TE = T - 20, TH = TE / 2;
+  static_assert(TH % 2 == 0 && TH + 2 * HW <= T, "half-tile geometry");
+  __shared__ __attribute__((aligned(16)))
+  double lds[NLGeo<NP, kNLAdjW>::kLds + 8 + (BURG ? T * NP : 0)];
+  const int n = *count;  // final: k_adj_nl has completed
+  for (int i = blockIdx.x; i < 2 * n; i += gridDim.x) {
+    if (i != int(blockIdx.x)) __syncthreads();  // the previous item's LDS reads are done
+    const int64_t tile = list[i / 2];
+    const int64_t e0 = tile * TE + (i & 1) * TH - HW;
+    if (edge_tile(e0, T, args.ktot, args.K))
+      nl_adj_tile<NP, BURG, LIM, UNI, true, true, HW, false>(lds, e0, TH, win, wout, snap, eta,
+                                                             scale, codes, args);
+    else
+      nl_adj_tile<NP, BURG, LIM, UNI, true, false, HW, false>(lds, e0, TH, win, wout, snap, eta,
+                                                              scale, codes, args);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -825,8 +881,8 @@ int launch_step_nl(const dg_plan* p, const double* in, double* snap, double* las
 
 template <int NP, bool BURG, bool LIM>
 int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const double* snap,
-                  double* eta, int em, const uint16_t* codes, double t_n, double src, double dt,
-                  hipStream_t st) {
+                  double* eta, int em, const uint16_t* codes, int32_t* count, double t_n,
+                  double src, double dt, hipStream_t st) {
   NLAdjArgs<NP> a;
   make_eo<NP>(p, p->uniform ? dt * p->s_uniform : dt, &a.op);  // see launch_step_nl
   for (int k = 0; k < EOArgs<NP>::NO * EOArgs<NP>::NE; ++k) a.qoe_h[k] = 0.5 * a.op.Qoe[k];
@@ -839,23 +895,37 @@ int launch_adj_nl(const dg_plan* p, const double* win, double* wout, const doubl
   a.K = int32_t(p->K);
   a.has_eta = eta != nullptr ? (em | kEtaOn) : 0;
   a.xcd = p->xcd_order;
-  constexpr int TE = kBlock * kNLAdjW - 20 * cone_per_stage<LIM>();
-  const unsigned grid = grid_for(p->ktot, TE);
   // the recorded decisions are only kept with a limiter (without one there are none)
   const bool known = LIM && codes != nullptr;
+  // tiles of the narrow cone with the record (k_adj_nl), else of the kernel's cone
+  const int TE = kBlock * kNLAdjW - 20 * (known ? 1 : cone_per_stage<LIM>());
+  const unsigned grid = grid_for(p->ktot, TE);
+  int32_t* list = known ? p->d_nl_list : nullptr;
+  if (known && (list == nullptr || count == nullptr || p->nl_list_tiles < int64_t(grid)))
+    return fail(DG_ERR_ARG, "config-3 adjoint: tile list not sized (nl_adj)");
   if (p->uniform && known)
     hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, true, true>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
-                       win, wout, snap, eta, p->d_scale, codes, a);
+                       win, wout, snap, eta, p->d_scale, codes, list, count, a);
   else if (p->uniform)
     hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, true, false>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
-                       win, wout, snap, eta, p->d_scale, codes, a);
+                       win, wout, snap, eta, p->d_scale, codes, list, count, a);
   else if (known)
     hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, false, true>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
-                       win, wout, snap, eta, p->d_scale, codes, a);
+                       win, wout, snap, eta, p->d_scale, codes, list, count, a);
   else
     hipLaunchKernelGGL((k_adj_nl<NP, BURG, LIM, false, false>), dim3(grid), dim3(kBlock * kNLAdjW), 0, st,
-                       win, wout, snap, eta, p->d_scale, codes, a);
+                       win, wout, snap, eta, p->d_scale, codes, list, count, a);
   HIP_TRY(hipGetLastError());
+  if (known) {
+    const unsigned gw = std::min<unsigned>(grid, unsigned(p->cu_count));
+    if (p->uniform)
+      hipLaunchKernelGGL((k_adj_nl_wide<NP, BURG, LIM, true>), dim3(gw), dim3(kBlock * kNLAdjW), 0,
+                         st, win, wout, snap, eta, p->d_scale, codes, list, count, a);
+    else
+      hipLaunchKernelGGL((k_adj_nl_wide<NP, BURG, LIM, false>), dim3(gw), dim3(kBlock * kNLAdjW),
+                         0, st, win, wout, snap, eta, p->d_scale, codes, list, count, a);
+    HIP_TRY(hipGetLastError());
+  }
   return DG_OK;
 }
 
@@ -877,13 +947,17 @@ int step_np(const dg_plan* p, int ms, const double* in, double* snap, double* la
 
 template <int NP>
 int adj_np(const dg_plan* p, const double* win, double* wout, const double* snap, double* eta,
-           int em, const uint16_t* codes, double t_n, double src, double dt, hipStream_t st) {
+           int em, const uint16_t* codes, int32_t* count, double t_n, double src, double dt,
+           hipStream_t st) {
   const bool burg = p->flux == DG_FLUX_BURGERS, lim = p->limiter != 0;
   if (burg && lim)
-    return launch_adj_nl<NP, true, true>(p, win, wout, snap, eta, em, codes, t_n, src, dt, st);
+    return launch_adj_nl<NP, true, true>(p, win, wout, snap, eta, em, codes, count, t_n, src, dt,
+                                         st);
   if (burg)
-    return launch_adj_nl<NP, true, false>(p, win, wout, snap, eta, em, codes, t_n, src, dt, st);
-  return launch_adj_nl<NP, false, true>(p, win, wout, snap, eta, em, codes, t_n, src, dt, st);
+    return launch_adj_nl<NP, true, false>(p, win, wout, snap, eta, em, codes, count, t_n, src,
+                                          dt, st);
+  return launch_adj_nl<NP, false, true>(p, win, wout, snap, eta, em, codes, count, t_n, src, dt,
+                                        st);
 }
 
 int launch_nl_step(const dg_plan* p, int ms, const double* in, double* snap, double* last,
@@ -965,6 +1039,30 @@ int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
   std::vector<double> tn(size_t(nsteps) + 1);
   tn[0] = t0;
   for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  // k_adj_nl's troubled-tile list (shared by the steps: each step's wide pass has finished
+  // before the next step lists) and one count per step, zeroed here once per sweep
+  int32_t* counts = nullptr;
+  if (decisions && p->limiter && nsteps > 0) {
+    constexpr int64_t te = kBlock * kNLAdjW - 20;  // k_adj_nl's narrow-cone tile outputs
+    const int64_t need = (p->ktot + te - 1) / te;
+    if (p->nl_list_tiles < need || p->nl_list_steps < nsteps) {
+      HIP_TRY(hipStreamSynchronize(st));  // an earlier sweep may still use it
+      (void)hipFree(p->d_nl_list);
+      p->d_nl_list = nullptr;
+      p->nl_list_tiles = p->nl_list_steps = 0;
+      const int64_t cap = (int64_t(p->K_cap) * p->batch + te - 1) / te;
+      const int64_t tiles = cap > need ? cap : need;
+      const int64_t steps = nsteps > 64 ? nsteps : 64;
+      if (hipMalloc(&p->d_nl_list, sizeof(int32_t) * (tiles + steps)) != hipSuccess) {
+        p->d_nl_list = nullptr;
+        return fail(DG_ERR_NOMEM, "hipMalloc of the config-3 adjoint's tile list failed");
+      }
+      p->nl_list_tiles = tiles;
+      p->nl_list_steps = steps;
+    }
+    counts = p->d_nl_list + p->nl_list_tiles;
+    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int32_t) * nsteps, st));
+  }
   // Launch for step n reads w^{n+1} and u^n and writes w^n; intermediate states alternate
   // between the plan scratch fields and the last launch lands in w.  (w may alias the
   // terminal snapshot: only the first launch reads w, and no launch reads snapshot nsteps.)
@@ -979,7 +1077,8 @@ int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt,
     int rc = DG_OK;
     const uint16_t* dec = decisions ? decisions + int64_t(n) * p->ktot : nullptr;
     DG_DISPATCH_NP(p->NP, rc = adj_np<NP>(p, in, out, snapshots + int64_t(n) * field, eta, em,
-                                          dec, tn[n], src, dt, st));
+                                          dec, counts ? counts + n : nullptr, tn[n], src, dt,
+                                          st));
     if (rc) return rc;
     in = out;
   }

@@ -450,6 +450,8 @@ struct dg_plan {
   // states, indicator partials; grown on demand) and the switch (1: one dataflow launch where
   // the shape allows it, 0: the launch-per-block pair)
   void* d_sweep = nullptr;
+  int32_t* d_nl_list = nullptr;  // config-3 adjoint's troubled-tile list + per-step counts
+  int64_t nl_list_tiles = 0, nl_list_steps = 0;
   size_t sweep_bytes = 0;
   size_t sweep_sync = 0;  // bytes of its control region (zeroed, then kept by epochs)
   int64_t sweep_items = -1;  // work items of the last dataflow launch on that region

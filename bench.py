@@ -483,7 +483,8 @@ def main_config3(args, world, rank, dev):
                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_bytes / (adj_m * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                    "kernel": f"k_adj_nl<{Np},burgers,limiter,nonuniform> (1 reverse step + "
-                             f"stage recompute + DWR per launch)",
+                             f"stage recompute + DWR per launch, tiles on the narrow cone; "
+                             f"+ k_adj_nl_wide for tiles with a troubled cell)",
                    "launch_us": adj_m, "launch_us_stats": stats(adj_us),
                    "algorithmic_bytes": adj_bytes},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_bytes / (fwd_m * 1e-6) / 1e9,
@@ -508,7 +509,13 @@ def main_config3(args, world, rank, dev):
   if prof and prof.get("N") == N and prof.get("K") == K:
     uni = "false"  # after its first split the refine loop's mesh is non-uniform
     pk = {k: v for k, v in prof["kernels"].items() if f", {uni}," in k or k.endswith(f", {uni}>")}
-    ka = next((v for k, v in pk.items() if k.startswith("k_adj_nl")), None)
+    ka = next((v for k, v in pk.items() if k.startswith("k_adj_nl<")), None)
+    kw = next((v for k, v in pk.items() if k.startswith("k_adj_nl_wide<")), None)
+    if ka and kw:  # one wide-cone pass per reverse step: count its bytes and flops with it
+      ka = dict(ka)
+      for key in ("hbm_bytes_per_launch", "fp64_flops_issued_per_launch"):
+        if key in ka and key in kw:
+          ka[key] += kw[key]
     kf = next((v for k, v in pk.items() if k.startswith("k_step_nl") and k.endswith(f", {ms}>")), None)
     src = prof.get("source")
     if ka and "hbm_bytes_per_launch" in ka:

@@ -96,3 +96,45 @@ def test_record_is_validated(pkg, gpu):
   with pytest.raises(TypeError):
     op.forward(snaps[0], 0.0, 1e-4, 2, snaps,
                decisions=torch.zeros(100, dtype=torch.int32, device=gpu))
+
+
+@pytest.mark.parametrize("limit,N,K,uniform", [
+    ("1", 2, 150000, True),     # every cell troubled: every tile on the wide cone
+    (True, 4, 200000, False),   # a jump every 400 elements: wide and narrow tiles side by side
+])
+def test_troubled_tiles_on_the_wide_cone(pkg, gpu, limit, N, K, uniform):
+  """The record-driven adjoint lays its tiles out for the narrow cone (no troubled cell) and
+  lists the others for k_adj_nl_wide, which recomputes them as half tiles on the wide cone
+  (grid-stride over the list, the list reset by its last workgroup for the next step).  With
+  more listed tiles than the wide launch has workgroups, over several steps, the result
+  equals the re-testing adjoint bit for bit."""
+  import torch
+  rng = np.random.default_rng(K)
+  v_x = None if uniform else refined_vx(K, rng)
+  S, mesh, op = setup(pkg, N, K, v_x=v_x, flux="burgers", limiter=limit)
+  K = S["K"]
+  dt = oadv.bench_dt(S)
+  nsteps = 3
+  x = S["x"]
+  u0 = np.sin(2 * np.pi * x) + np.floor(x * (K / 400.0)) % 2
+  snaps = op.new_field(nsteps + 1)
+  rec = torch.zeros(nsteps * K, dtype=torch.int16, device=gpu)
+  op.forward(dev(setup1d.to_elem_major(u0), gpu), 0.0, dt, nsteps, snaps, decisions=rec)
+  te = 236  # k_adj_nl's narrow-cone tile outputs
+  codes = host(rec).reshape(nsteps, K)
+  for n in range(nsteps):
+    tiles = np.zeros(-(-K // te), dtype=bool)
+    lo = np.maximum(np.arange(len(tiles)) * te - 10, 0)
+    for t in range(len(tiles)):
+      tiles[t] = codes[n, lo[t]:t * te + te + 10].any()
+    assert tiles.sum() > 256  # more (tile, half) items than 2 x CUs
+    if limit is True:
+      assert not tiles.all()
+  res = []
+  for d in (None, rec):
+    w = snaps[nsteps].clone()
+    eta = torch.zeros(K, dtype=torch.float64, device=gpu)
+    op.adjoint(w, snaps, 0.0, dt, nsteps, src_coef=0.3, eta=eta, decisions=d)
+    res.append((host(w), host(eta)))
+  np.testing.assert_array_equal(res[0][0], res[1][0])
+  np.testing.assert_array_equal(res[0][1], res[1][1])
