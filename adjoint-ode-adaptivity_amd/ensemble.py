@@ -245,20 +245,23 @@ class DeviceReducer:
   def argmax(self, x):
     return self.op.argmax_ex(x.contiguous(), self.idx, self.value, self.nonfinite, use_abs=True)
 
-  def argmax_value(self, x):
-    """(index, |x[index]|) of argmax |x| as (1,) device tensors, state untouched."""
-    i = torch.empty(1, dtype=torch.int64, device=self.op.device)
-    v = torch.empty(1, dtype=torch.float64, device=self.op.device)
-    self.op.argmax_ex(x.contiguous(), i, v, None, use_abs=True)
-    return i, v
+  def candidate(self, x, offset=0):
+    """This rank's refine candidate as a device int64[2]: the bits of |x[i]| (float64) and
+    i + offset, i = argmax |x| (numpy order), written by dg_argmax_ex; state untouched."""
+    c = torch.empty(2, dtype=torch.int64, device=self.op.device)
+    self.op.argmax_ex(x.contiguous(), c[1:2], c[0:1].view(torch.float64), None, use_abs=True)
+    if offset:
+      c[1:2].add_(offset)
+    return c
 
-  def finish(self, values, indices):
-    """The refine decision from per-rank candidates (values (W,) float64, indices (W,) int64,
-    rank order): the argmax of the values under numpy's order (ties to the lowest rank, which
-    owns the lowest indices) into the state, then its index."""
+  def finish(self, cands):
+    """The refine decision from the ranks' candidates (W, 2) int64 in rank order: the argmax
+    of the values under numpy's order (ties to the lowest rank, which owns the lowest
+    indices) into the state, then its index."""
     w = torch.empty(1, dtype=torch.int64, device=self.op.device)
-    self.op.argmax_ex(values.contiguous(), w, self.value, self.nonfinite, use_abs=False)
-    torch.index_select(indices.contiguous(), 0, w, out=self.idx)
+    vals = cands[:, 0].contiguous().view(torch.float64)
+    self.op.argmax_ex(vals, w, self.value, self.nonfinite, use_abs=False)
+    torch.index_select(cands[:, 1], 0, w, out=self.idx)
     return self.idx
 
 
@@ -323,8 +326,11 @@ def refine_decision(partial, n_total, reducer, group=None):
     return gather_indicator(partial, n_total, reducer, group)[1]
   K = partial.numel()
   chunk = -(-K // world)
-  send = partial.new_zeros(world * chunk)
-  send[:K] = partial.reshape(-1)
+  if K == world * chunk and partial.is_contiguous():
+    send = partial.reshape(-1)  # no padding needed: no copy
+  else:
+    send = partial.new_zeros(world * chunk)
+    send[:K] = partial.reshape(-1)
   recv = _exchange(dist.all_to_all_single, send, group)
   mine = reducer.sum_rows(recv.view(world, chunk))  # rank order
   lo = rank * chunk
@@ -332,13 +338,12 @@ def refine_decision(partial, n_total, reducer, group=None):
   if n > 0:
     sl = mine[:n]
     mean = sl / float(n_total) if n_total != 1 else sl
-    i, v = reducer.argmax_value(mean)
-    cand = torch.cat([v.reshape(1).view(torch.int64), i.reshape(1) + lo])
+    cand = reducer.candidate(mean, lo)
   else:  # a rank past the end of K: the weakest candidate
     cand = torch.tensor([np.array([-np.inf]).view(np.int64)[0], np.iinfo(np.int64).max],
                         dtype=torch.int64, device=partial.device)
-  allc = _exchange(dist.all_gather_into_tensor, cand.contiguous(), group, 2 * world).view(world, 2)
-  return reducer.finish(allc[:, 0].contiguous().view(torch.float64), allc[:, 1].contiguous())
+  allc = _exchange(dist.all_gather_into_tensor, cand, group, 2 * world).view(world, 2)
+  return reducer.finish(allc)
 
 
 _KEEP = {}

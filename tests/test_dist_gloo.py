@@ -25,16 +25,18 @@ class OracleReducer:
     from oracle import adjoint as oadj
     return torch.tensor([oadj.argmax(x.numpy(), use_abs=True)])
 
-  def argmax_value(self, x):
+  def candidate(self, x, offset=0):
     from oracle import adjoint as oadj
     i = oadj.argmax(x.numpy(), use_abs=True)
-    return torch.tensor([i]), torch.tensor([abs(float(x[i]))], dtype=torch.float64)
+    v = np.array([abs(float(x[i]))]).view(np.int64)[0]
+    return torch.tensor([v, i + offset], dtype=torch.int64)
 
-  def finish(self, values, indices):
+  def finish(self, cands):
     from oracle import adjoint as oadj
+    values = cands[:, 0].contiguous().view(torch.float64)
     w = oadj.argmax(values.numpy())
     self.value = float(values[w])
-    return indices[w:w + 1].clone()
+    return cands[w:w + 1, 1].clone()
 
 
 def _free_port():

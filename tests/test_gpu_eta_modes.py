@@ -137,7 +137,7 @@ def test_stream_copy_rejects_misaligned(pkg, gpu):
 
 @pytest.mark.parametrize("kind", ["rand", "tie", "nan"])
 def test_device_reducer_candidates_pick_the_full_argmax(pkg, gpu, kind):
-  """DeviceReducer.argmax_value / finish, the device half of ensemble.refine_decision: the
+  """DeviceReducer.candidate / finish, the device half of ensemble.refine_decision: the
   per-slice (value, global index) candidates of W ranks, reduced in rank order, give the
   index and value of numpy's argmax of |x| over the whole vector (the collectives around
   them are covered on CPU by tests/test_dist_gloo.py)."""
@@ -152,13 +152,11 @@ def test_device_reducer_candidates_pick_the_full_argmax(pkg, gpu, kind):
   elif kind == "nan":
     x[[100, 8000]] = [1e6, np.nan]
   chunk = -(-K // W)
-  vals, idxs = [], []
+  cands = []
   for r in range(W):
     sl = torch.tensor(x[r * chunk:(r + 1) * chunk], device=gpu)
-    i, v = red.argmax_value(sl)
-    vals.append(v)
-    idxs.append(i + r * chunk)
-  out = red.finish(torch.cat(vals), torch.cat(idxs))
+    cands.append(red.candidate(sl, r * chunk))
+  out = red.finish(torch.stack(cands))
   torch.cuda.synchronize()
   want = oadj.argmax(x, use_abs=True)
   assert int(out[0]) == int(red.idx[0]) == want
