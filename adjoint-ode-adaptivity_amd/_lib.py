@@ -80,6 +80,8 @@ SIGNATURES = {
     "dg_stream_copy": (_i32, [_vp, _vp, _i64, _vp]),
     "dg_host_alias": (_i32, [_vp, ctypes.POINTER(_vp)]),
     "dg_sum_rows": (_i32, [_vp, _i64, _i64, _vp, _vp]),
+    "dg_slice_candidate": (_i32, [_vp, _vp, _i64, _i64, _i64, ctypes.c_double, _i64, _vp, _vp]),
+    "dg_candidates_argmax": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp]),
     "dg_init_sine": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "dg_time_march": (_i32, [_i32, _i32, _vp, _vp, _vp, _i32, _vp, _i64, _vp, ctypes.c_double,
                              _i32, _vp, _vp, _vp]),

@@ -756,6 +756,78 @@ __global__ __launch_bounds__(kBlock) void k_sum_rows(const double* __restrict__ 
   out[k] = acc;
 }
 
+// dg_slice_candidate: the rank's mean slice, never stored: summed and divided per element,
+// in k_sum_rows' order, straight into the argmax partials.
+__global__ __launch_bounds__(kBlock) void k_slice_partial(const double* __restrict__ x,
+                                                          int64_t rows, int64_t n, int64_t ld,
+                                                          double divisor,
+                                                          double* __restrict__ pv,
+                                                          int64_t* __restrict__ pi) {
+  double bv = 0.0;
+  int64_t bi = -1;
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+    double acc = x[i];
+    for (int64_t r = 1; r < rows; ++r) acc = acc + x[r * ld + i];
+    const double v = fabs(divisor != 1.0 ? acc / divisor : acc);
+    if (bi < 0 || better(v, i, bv, bi)) {
+      bv = v;
+      bi = i;
+    }
+  }
+  if (bi < 0) {
+    bv = -INFINITY;
+    bi = INT64_MAX;
+  }
+  block_argmax(bv, bi);
+  if (threadIdx.x == 0) {
+    pv[blockIdx.x] = bv;
+    pi[blockIdx.x] = bi;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_slice_final(const double* __restrict__ pv,
+                                                        const int64_t* __restrict__ pi,
+                                                        int nparts, int64_t offset,
+                                                        int64_t* __restrict__ cand) {
+  double bv = -INFINITY;
+  int64_t bi = INT64_MAX;
+  for (int p = threadIdx.x; p < nparts; p += kBlock) {
+    if (better(pv[p], pi[p], bv, bi)) {
+      bv = pv[p];
+      bi = pi[p];
+    }
+  }
+  block_argmax(bv, bi);
+  if (threadIdx.x == 0) {
+    cand[0] = __double_as_longlong(bv);
+    cand[1] = bi + offset;
+  }
+}
+
+// dg_candidates_argmax: one block over the w (value bits, index) pairs; a candidate's
+// position is its tie-break key (ranks own ascending index ranges).
+__global__ __launch_bounds__(kBlock) void k_candidates(const int64_t* __restrict__ cands,
+                                                       int64_t w, int64_t* __restrict__ idx,
+                                                       double* __restrict__ val,
+                                                       int64_t* __restrict__ nonfinite) {
+  double bv = -INFINITY;
+  int64_t bp = INT64_MAX;
+  for (int64_t p = threadIdx.x; p < w; p += kBlock) {
+    const double v = __longlong_as_double(cands[2 * p]);
+    if (better(v, p, bv, bp)) {
+      bv = v;
+      bp = p;
+    }
+  }
+  block_argmax(bv, bp);
+  if (threadIdx.x == 0) {
+    idx[0] = cands[2 * bp + 1];
+    if (val != nullptr) val[0] = bv;
+    if (nonfinite != nullptr && !isfinite(bv)) nonfinite[0] += 1;
+  }
+}
+
 template <int NP>
 __global__ __launch_bounds__(kBlock) void k_init_sine(const double* __restrict__ VX,
                                                       const double* __restrict__ amp,
@@ -1905,6 +1977,35 @@ int dg_sum_rows(const double* x, int64_t rows, int64_t n, double* out, void* str
   if (rows < 1 || n < 1) return fail(DG_ERR_ARG, "rows and n must be >= 1");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_sum_rows, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, x, rows, n, out);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+int dg_slice_candidate(dg_plan* p, const double* x, int64_t rows, int64_t n, int64_t ld,
+                       double divisor, int64_t offset, int64_t* cand, void* stream) {
+  if (!p || !x || !cand) return fail(DG_ERR_ARG, "null argument");
+  if (rows < 1 || n < 1 || ld < n) return fail(DG_ERR_ARG, "rows, n >= 1 and ld >= n required");
+  if (n > p->ktot * p->NP) return fail(DG_ERR_ARG, "n out of range");
+  if (!(divisor > 0.0)) return fail(DG_ERR_ARG, "divisor must be positive");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t parts = (n + 4 * kBlock - 1) / (4 * kBlock);
+  if (parts > kArgmaxParts) parts = kArgmaxParts;
+  hipLaunchKernelGGL(k_slice_partial, dim3(unsigned(parts)), dim3(kBlock), 0, st, x, rows, n, ld,
+                     divisor, p->d_pv, p->d_pi);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_slice_final, dim3(1), dim3(kBlock), 0, st, p->d_pv, p->d_pi, int(parts),
+                     offset, cand);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+int dg_candidates_argmax(const int64_t* cands, int64_t w, int64_t* idx, double* value,
+                         int64_t* nonfinite_count, void* stream) {
+  if (!cands || !idx) return fail(DG_ERR_ARG, "null argument");
+  if (w < 1) return fail(DG_ERR_ARG, "w must be >= 1");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_candidates, dim3(1), dim3(kBlock), 0, st, cands, w, idx, value,
+                     nonfinite_count);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }

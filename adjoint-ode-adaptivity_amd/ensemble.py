@@ -17,7 +17,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .operators import DGAdvection1D, DWREstimate, sum_rows
+from .operators import DGAdvection1D, DWREstimate, candidates_argmax, sum_rows
 
 
 def ic_params(indices, seed_base=0):
@@ -245,24 +245,18 @@ class DeviceReducer:
   def argmax(self, x):
     return self.op.argmax_ex(x.contiguous(), self.idx, self.value, self.nonfinite, use_abs=True)
 
-  def candidate(self, x, offset=0):
-    """This rank's refine candidate as a device int64[2]: the bits of |x[i]| (float64) and
-    i + offset, i = argmax |x| (numpy order), written by dg_argmax_ex; state untouched."""
+  def candidate(self, slices, n, divisor, offset):
+    """This rank's refine candidate as a device int64[2] (the bits of |m[i]| and i + offset,
+    m = the slices' rank-order sum over the first n columns / divisor, i = argmax |m|):
+    dg_slice_candidate, two launches, state untouched."""
     c = torch.empty(2, dtype=torch.int64, device=self.op.device)
-    self.op.argmax_ex(x.contiguous(), c[1:2], c[0:1].view(torch.float64), None, use_abs=True)
-    if offset:
-      c[1:2].add_(offset)
-    return c
+    return self.op.slice_candidate(slices.contiguous(), n, divisor, offset, c)
 
   def finish(self, cands):
     """The refine decision from the ranks' candidates (W, 2) int64 in rank order: the argmax
     of the values under numpy's order (ties to the lowest rank, which owns the lowest
-    indices) into the state, then its index."""
-    w = torch.empty(1, dtype=torch.int64, device=self.op.device)
-    vals = cands[:, 0].contiguous().view(torch.float64)
-    self.op.argmax_ex(vals, w, self.value, self.nonfinite, use_abs=False)
-    torch.index_select(cands[:, 1], 0, w, out=self.idx)
-    return self.idx
+    indices) into the state (dg_candidates_argmax), then its index."""
+    return candidates_argmax(cands.contiguous(), self.idx, self.value, self.nonfinite)
 
 
 def _exchange(coll, send, group, n_out=None):
@@ -332,13 +326,10 @@ def refine_decision(partial, n_total, reducer, group=None):
     send = partial.new_zeros(world * chunk)
     send[:K] = partial.reshape(-1)
   recv = _exchange(dist.all_to_all_single, send, group)
-  mine = reducer.sum_rows(recv.view(world, chunk))  # rank order
   lo = rank * chunk
   n = max(0, min(chunk, K - lo))
-  if n > 0:
-    sl = mine[:n]
-    mean = sl / float(n_total) if n_total != 1 else sl
-    cand = reducer.candidate(mean, lo)
+  if n > 0:  # the rank-order sum of the received slices, its mean and argmax in one pass
+    cand = reducer.candidate(recv.view(world, chunk), n, float(n_total), lo)
   else:  # a rank past the end of K: the weakest candidate
     cand = torch.tensor([np.array([-np.inf]).view(np.int64)[0], np.iinfo(np.int64).max],
                         dtype=torch.int64, device=partial.device)

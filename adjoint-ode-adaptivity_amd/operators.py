@@ -436,6 +436,21 @@ class DGAdvection1D:
     _lib.check(rc, "dg_argmax_ex")
     return idx
 
+  def slice_candidate(self, x, n, divisor, offset, cand):
+    """This rank's refine candidate from its received slices x (rows, ld) CUDA float64:
+    cand (CUDA int64[2]) = (bits of |m[i]|, i + offset), m = the rows' ascending sum over the
+    first n columns / divisor, i = argmax |m| (dg_slice_candidate; no host sync)."""
+    if not x.is_cuda or x.dtype != torch.float64 or x.dim() != 2 or not x.is_contiguous():
+      raise TypeError("x must be a contiguous 2-D CUDA float64 tensor")
+    if not cand.is_cuda or cand.dtype != torch.int64 or cand.numel() < 2:
+      raise TypeError("cand must be a CUDA int64 tensor of 2 elements")
+    rows, ld = x.shape
+    rc = self._lib.dg_slice_candidate(self._plan, ctypes.c_void_p(x.data_ptr()), int(rows),
+                                      int(n), int(ld), float(divisor), int(offset),
+                                      ctypes.c_void_p(cand.data_ptr()), _stream(self.device))
+    _lib.check(rc, "dg_slice_candidate")
+    return cand
+
   def init_sine(self, amp, freq, phase, out=None):
     """u_b(x) = amp[b] sin(2 pi freq[b] x + phase[b]) on the device (ensemble ICs)."""
     out = self.new_field() if out is None else out
@@ -562,3 +577,16 @@ def sum_rows(x, rows, out=None):
                        ctypes.c_void_p(out.data_ptr()), _stream(x.device))
   _lib.check(rc, "dg_sum_rows")
   return out
+
+
+def candidates_argmax(cands, idx, value=None, nonfinite=None):
+  """The refine decision from the ranks' candidates (CUDA int64 (W, 2), rank order) into idx
+  (and value / +1 nonfinite) on the device (dg_candidates_argmax)."""
+  lib = _lib.load()
+  if not cands.is_cuda or cands.dtype != torch.int64 or not cands.is_contiguous():
+    raise TypeError("cands must be a contiguous CUDA int64 tensor")
+  ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+  rc = lib.dg_candidates_argmax(ctypes.c_void_p(cands.data_ptr()), cands.numel() // 2, ptr(idx),
+                                ptr(value), ptr(nonfinite), _stream(cands.device))
+  _lib.check(rc, "dg_candidates_argmax")
+  return idx

@@ -353,6 +353,23 @@ int dg_host_alias(void* host, void** device);
  * Ensemble reduction of per-IC indicators (python/Main_width_ref.py:479 mean-over-ICs role). */
 int dg_sum_rows(const double* x, int64_t rows, int64_t n, double* out, void* stream);
 
+/* One rank's refine candidate in a multi-rank ensemble (python/Main_width_ref.py:479,491: the
+ * argmax of the mean indicator's magnitude, computed slice by slice): the mean
+ * m[k] = (sum_{r=0}^{rows-1} x[r*ld + k]) / divisor for k < n (rows summed in ascending r,
+ * as dg_sum_rows; divisor 1 skips the division, which would be exact), then i = argmax |m|
+ * under numpy's order, written as cand[0] = the bits of |m[i]| (a double) and
+ * cand[1] = i + offset (device int64[2]).  n <= batch*K*Np of the plan. */
+int dg_slice_candidate(dg_plan* plan, const double* x, int64_t rows, int64_t n, int64_t ld,
+                       double divisor, int64_t offset, int64_t* cand, void* stream);
+
+/* The refine decision from the ranks' candidates (cands: device int64[w][2] in rank order, as
+ * dg_slice_candidate writes them): the winner is the argmax of the values under numpy's
+ * order (NaN first, ties to the lowest rank); idx[0] = its index, value[0] (nullable) = its
+ * value, nonfinite_count[0] (nullable) += 1 when that value is not finite -- dg_argmax_ex's
+ * outputs for the whole vector, bit for bit. */
+int dg_candidates_argmax(const int64_t* cands, int64_t w, int64_t* idx, double* value,
+                         int64_t* nonfinite_count, void* stream);
+
 /* Synthetic ensemble initial conditions u_b(x) = amp[b] * sin(2*pi*freq[b]*x + phase[b])
  * on the plan's mesh (amp/freq/phase: device arrays of length batch). */
 int dg_init_sine(const dg_plan* plan, const double* amp, const double* freq,

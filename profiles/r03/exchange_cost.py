@@ -1,7 +1,8 @@
 """Device-side cost of ensemble.refine_decision's per-step work at W ranks on ONE GPU (no
-collective): the rank's sum of the W received slices (dg_sum_rows), the mean, its candidate
-(dg_argmax_ex) and the reduction of W gathered candidates (dg_argmax_ex + index_select),
-against gather_indicator's (sum, mean of the full vector, argmax).  K = 2^20 (config 2's
+collective): the rank's candidate from the W received slices (dg_slice_candidate: rank-order
+sum, mean and argmax in one pass) and the reduction of W gathered candidates
+(dg_candidates_argmax), against gather_indicator's (dg_sum_rows of the slices, mean of the
+full vector, argmax).  K = 2^20 (config 2's
 weak-scaling indicator), W = 2, 4, 8.  The RCCL all-to-all / all-gather themselves are not
 measurable on a one-GPU box.  "_eager" is the host-issue-bound loop, "_gpu" the same work
 replayed from a HIP graph (the GPU's own time)."""
@@ -25,13 +26,12 @@ for W in (2, 4, 8):
   full = torch.rand(W, K, dtype=torch.float64, device=dev)
 
   def decision():
-    mine = red.sum_rows(recv)
-    mean = mine / float(W)
-    c = red.candidate(mean, chunk)
+    c = red.candidate(recv, chunk, float(W), chunk)
     allc = torch.stack([c] * W)  # stands in for the gathered (W, 2) block
     red.finish(allc)
 
-  def gather():  # gather_indicator's local work after its exchanges (full-length mean)
+  def gather():  # gather_indicator's local work around its exchanges
+    mine = red.sum_rows(recv)
     mean = full[0] / float(W)
     red.argmax(mean)
 

@@ -25,10 +25,12 @@ class OracleReducer:
     from oracle import adjoint as oadj
     return torch.tensor([oadj.argmax(x.numpy(), use_abs=True)])
 
-  def candidate(self, x, offset=0):
+  def candidate(self, slices, n, divisor, offset):
     from oracle import adjoint as oadj
-    i = oadj.argmax(x.numpy(), use_abs=True)
-    v = np.array([abs(float(x[i]))]).view(np.int64)[0]
+    m = oadj.sum_rows(slices.numpy())[:n]
+    m = m / divisor if divisor != 1 else m
+    i = oadj.argmax(m, use_abs=True)
+    v = np.array([abs(float(m[i]))]).view(np.int64)[0]
     return torch.tensor([v, i + offset], dtype=torch.int64)
 
   def finish(self, cands):

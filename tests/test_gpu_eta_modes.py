@@ -135,30 +135,42 @@ def test_stream_copy_rejects_misaligned(pkg, gpu):
     pkg.operators.stream_copy(src[1:], dst[1:])
 
 
-@pytest.mark.parametrize("kind", ["rand", "tie", "nan"])
-def test_device_reducer_candidates_pick_the_full_argmax(pkg, gpu, kind):
-  """DeviceReducer.candidate / finish, the device half of ensemble.refine_decision: the
-  per-slice (value, global index) candidates of W ranks, reduced in rank order, give the
-  index and value of numpy's argmax of |x| over the whole vector (the collectives around
-  them are covered on CPU by tests/test_dist_gloo.py)."""
+@pytest.mark.parametrize("kind,n_total", [("rand", 3), ("tie", 4), ("nan", 3), ("signed", 1)])
+def test_device_reducer_candidates_pick_the_full_argmax(pkg, gpu, kind, n_total):
+  """DeviceReducer.candidate / finish (dg_slice_candidate, dg_candidates_argmax), the device
+  half of ensemble.refine_decision: each of W ranks sums the W rows it received for its slice
+  in rank order, divides by the IC count and takes its argmax candidate; the candidates,
+  reduced in rank order, give the index and value of numpy's argmax of |mean| over the whole
+  vector bit for bit (the collectives around them are covered on CPU by
+  tests/test_dist_gloo.py).  K not a multiple of W: the last slice is short."""
   import torch
   K, W = 10007, 4
   mesh = pkg.BaseGalerkin1D(n=2, k=K)
   red = pkg.ensemble.DeviceReducer(pkg.operators.DGAdvection1D(mesh))
   rng = np.random.default_rng(11)
-  x = np.abs(rng.standard_normal(K))
+  parts = rng.standard_normal((W, K)) * 10.0 ** rng.integers(-3, 3, (W, K))
+  if kind != "signed":
+    parts = np.abs(parts)
   if kind == "tie":
-    x[[9000, 2600, 2500]] = 7.0  # equal maxima in slices 3, 1, 0: the lowest index wins
+    parts[:, [9000, 2600, 2500]] = [[7e6], [1e6], [5e5], [5e5]]  # equal maximal sums in slices 3, 1, 0
   elif kind == "nan":
-    x[[100, 8000]] = [1e6, np.nan]
+    parts[2, 8000] = np.nan
+    parts[:, 100] = 1e6
+  total = oadj.sum_rows(parts)
+  mean = total / n_total if n_total != 1 else total
   chunk = -(-K // W)
+  padded = np.zeros((W, W * chunk))
+  padded[:, :K] = parts
   cands = []
   for r in range(W):
-    sl = torch.tensor(x[r * chunk:(r + 1) * chunk], device=gpu)
-    cands.append(red.candidate(sl, r * chunk))
+    recv = torch.tensor(np.ascontiguousarray(padded[:, r * chunk:(r + 1) * chunk]), device=gpu)
+    n = min(chunk, K - r * chunk)
+    cands.append(red.candidate(recv, n, float(n_total), r * chunk))
   out = red.finish(torch.stack(cands))
   torch.cuda.synchronize()
-  want = oadj.argmax(x, use_abs=True)
+  want = oadj.argmax(mean, use_abs=True)
   assert int(out[0]) == int(red.idx[0]) == want
-  np.testing.assert_array_equal(host(red.value), np.abs(x[want:want + 1]))
+  np.testing.assert_array_equal(host(red.value), np.abs(mean[want:want + 1]))
   assert int(red.nonfinite[0]) == (1 if kind == "nan" else 0)
+  if kind == "tie":
+    assert want == 2500
