@@ -763,21 +763,22 @@ __global__ __launch_bounds__(kBlock) void k_slice_partial(const double* __restri
                                                           double divisor,
                                                           double* __restrict__ pv,
                                                           int64_t* __restrict__ pi) {
-  double bv = 0.0;
-  int64_t bi = -1;
+  // Start from the weakest candidate (every |m| beats it) rather than k_argmax_partial's
+  // "no candidate yet" flag: with the flag, this loop (the division and the row loop in its
+  // body) compiled to code that kept the first element's value as the thread's best while
+  // still advancing its index (ROCm 7.2 clang, gfx950), seen on the GPU as argmaxes over the
+  // first grid-stride pass only.
+  double bv = -INFINITY;
+  int64_t bi = INT64_MAX;
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
     double acc = x[i];
     for (int64_t r = 1; r < rows; ++r) acc = acc + x[r * ld + i];
-    const double v = fabs(divisor != 1.0 ? acc / divisor : acc);
-    if (bi < 0 || better(v, i, bv, bi)) {
+    const double v = fabs(acc / divisor);  // (x / 1 == x exactly: no special case)
+    if (better(v, i, bv, bi)) {
       bv = v;
       bi = i;
     }
-  }
-  if (bi < 0) {
-    bv = -INFINITY;
-    bi = INT64_MAX;
   }
   block_argmax(bv, bi);
   if (threadIdx.x == 0) {
