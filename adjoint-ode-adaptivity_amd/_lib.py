@@ -24,6 +24,7 @@ DG_TUNE_REC_LANE_ELEMENTS, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 7, 8
 DG_TUNE_P_TILE_WIDTH, DG_TUNE_P_STEPS_PER_LAUNCH = 9, 10
 DG_TUNE_REC_FWD_TILE_WIDTH = 11
 DG_TUNE_REC_SWEEP = 12
+DG_TUNE_SWEEP_SPIN_LIMIT = 13
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2

@@ -686,19 +686,23 @@ __global__ __launch_bounds__(kBlock) void k_argmax_partial(const double* __restr
                                                            int64_t n, int use_abs,
                                                            double* __restrict__ pv,
                                                            int64_t* __restrict__ pi) {
-  double bv = 0.0;
-  int64_t bi = -1;
+  // Every thread starts from the weakest candidate (-inf, INT64_MAX): every element beats it
+  // under `better` (a -inf element by its lower index), so no "no candidate yet" flag is
+  // needed.  The flag form (bi = -1; `if (bi < 0 || better(...))`) is what ROCm 7.2's gfx950
+  // backend miscompiled in k_slice_partial: in the structurised divergent branch the copy for
+  // the not-taken edge of the phi of bv was placed where the lanes of the taken edge run it
+  // too, so a thread kept its first value as bv while bi advanced (DESIGN.md §5 "Support
+  // kernels"; the ISA and a reproducer: profiles/probes/argmax_phi_copy.hip).  This kernel's
+  // flag form happened to compile correctly; it no longer depends on that.
+  double bv = -INFINITY;
+  int64_t bi = INT64_MAX;
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
     const double v = use_abs ? fabs(x[i]) : x[i];
-    if (bi < 0 || better(v, i, bv, bi)) {
+    if (better(v, i, bv, bi)) {
       bv = v;
       bi = i;
     }
-  }
-  if (bi < 0) {  // thread saw nothing: weakest possible candidate
-    bv = -INFINITY;
-    bi = INT64_MAX;
   }
   block_argmax(bv, bi);
   if (threadIdx.x == 0) {
@@ -763,11 +767,11 @@ __global__ __launch_bounds__(kBlock) void k_slice_partial(const double* __restri
                                                           double divisor,
                                                           double* __restrict__ pv,
                                                           int64_t* __restrict__ pi) {
-  // Start from the weakest candidate (every |m| beats it) rather than k_argmax_partial's
-  // "no candidate yet" flag: with the flag, this loop (the division and the row loop in its
-  // body) compiled to code that kept the first element's value as the thread's best while
-  // still advancing its index (ROCm 7.2 clang, gfx950), seen on the GPU as argmaxes over the
-  // first grid-stride pass only.
+  // Start from the weakest candidate (every |m| beats it), as k_argmax_partial: with a "no
+  // candidate yet" flag this loop compiled to code that kept the first element's value as
+  // the thread's best while still advancing its index (ROCm 7.2, gfx950: a phi copy on a
+  // divergent edge, profiles/probes/argmax_phi_copy.hip), seen on the GPU as argmaxes over
+  // the first grid-stride pass only.
   double bv = -INFINITY;
   int64_t bi = INT64_MAX;
   const int64_t stride = int64_t(gridDim.x) * kBlock;
@@ -1166,11 +1170,13 @@ int sweep_scratch(dg_plan* p, size_t sync_bytes, size_t data_bytes, hipStream_t 
   const size_t sync = sync_bytes > p->sweep_sync ? sync_bytes : p->sweep_sync;
   if (!p->d_sweep || p->sweep_bytes < sync + data_bytes) {
     if (p->d_sweep) {
-      HIP_TRY(hipStreamSynchronize(st));  // an earlier sweep may still use it
-      (void)hipFree(p->d_sweep);
+      // Not freed: an earlier sweep may still run on it, and a HIP graph captured earlier
+      // keeps its addresses in the kernel arguments.  Retired until dg_plan_destroy.
+      p->sweep_retired.push_back(p->d_sweep);
       p->d_sweep = nullptr;
       p->sweep_bytes = p->sweep_sync = 0;
       p->sweep_items = -1;
+      p->sweep_sig = 0;
     }
     if (hipMalloc(&p->d_sweep, sync + data_bytes) != hipSuccess) {
       p->d_sweep = nullptr;
@@ -1363,7 +1369,10 @@ int dg_plan_destroy(dg_plan* p) {
   if (p->d_scratch2) (void)hipFree(p->d_scratch2);
   if (p->d_pv) (void)hipFree(p->d_pv);
   if (p->d_pi) (void)hipFree(p->d_pi);
+  if (p->d_sweep || !p->sweep_retired.empty()) (void)hipDeviceSynchronize();
   if (p->d_sweep) (void)hipFree(p->d_sweep);
+  for (void* q : p->sweep_retired) (void)hipFree(q);
+  if (p->h_sweep_err) (void)hipHostFree(p->h_sweep_err);
   if (p->d_nl_list) (void)hipFree(p->d_nl_list);
   delete p;
   return DG_OK;
@@ -1444,6 +1453,10 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       if (value != 1 && value != 2)
         return fail(DG_ERR_ARG, "record lane elements must be 1 or 2");
       p->rec_lane_elems = int(value);
+      return DG_OK;
+    case DG_TUNE_SWEEP_SPIN_LIMIT:
+      if (value < 0 || value > (1 << 30)) return fail(DG_ERR_ARG, "spin limit: 0 (default) .. 2^30");
+      p->sweep_spin_limit = int(value);
       return DG_OK;
     case DG_TUNE_REC_SWEEP:
       if (value != 0 && value != 1) return fail(DG_ERR_ARG, "record sweep mode must be 0 or 1");
@@ -1803,6 +1816,18 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
       return rc;
     return idx ? dg_argmax_ex(p, eta, p->ktot, 1, idx, value, nonfinite, stream) : DG_OK;
   }
+  if (p->h_sweep_err && *static_cast<volatile uint32_t*>(p->h_sweep_err) != 0u)
+    return fail(DG_ERR_HIP, "a dataflow sweep of this plan gave up waiting for a producer (its "
+                            "outputs were poisoned with NaN); dg_sweep_status clears the flag");
+  if (!p->h_sweep_err) {  // the watchdog's host-visible flag, mapped page-locked memory
+    void* h = nullptr;
+    HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
+    p->h_sweep_err = static_cast<uint32_t*>(h);
+    *p->h_sweep_err = 0u;
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
+    p->d_sweep_err = static_cast<uint32_t*>(d);
+  }
   const int nbF = nsteps / msf, nbA = nsteps / msa;
   const int64_t items = sweep_items(p, waves, msf, msa, nsteps);
   const size_t sync_bytes = (sizeof(uint32_t) * size_t(sweep_sync_words() + items) + 255) & ~size_t(255);
@@ -1817,10 +1842,15 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
                        sizeof(double) * size_t(p->ktot) * size_t(nparts) + 16 * size_t(am_parts);
   char* data = nullptr;
   if (const int rc = sweep_scratch(p, sync_bytes, bytes - sync_bytes, st, &data)) return rc;
-  if (p->sweep_items != items) {
-    // the take counter numbers launches by items per launch: a new shape starts it afresh
+  const uint64_t sig = uint64_t(items) * 1000003u ^ (uint64_t(waves) << 56) ^
+                      (uint64_t(msf) << 48) ^ (uint64_t(msa) << 40) ^ (uint64_t(nsteps) << 32) ^
+                      uint64_t(sweep_tiles_adj(p, waves, msa));
+  if (p->sweep_items != items || p->sweep_sig != sig) {
+    // the take counter numbers launches by items per launch and the fused refine's arrival
+    // counter by the last block's tiles: a new shape starts both afresh
     HIP_TRY(hipMemsetAsync(p->d_sweep, 0, sync_bytes, st));
     p->sweep_items = items;
+    p->sweep_sig = sig;
   }
   double* fld = reinterpret_cast<double*>(data);
   int next = 0;
@@ -1848,6 +1878,8 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   b.am_nf = nonfinite;
   b.am_pv = idx ? am : nullptr;
   b.am_pi = idx ? reinterpret_cast<int64_t*>(am + am_parts) : nullptr;
+  b.err_host = p->d_sweep_err;
+  b.spin_limit = p->sweep_spin_limit;
   const int mode = eta ? (kEtaOn | ((aflags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
                           ((aflags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
                        : 0;
@@ -1912,9 +1944,11 @@ int dg_sweep_status(dg_plan* p, int* status, void* stream) {
   uint32_t h = 0;
   HIP_TRY(hipMemcpyAsync(&h, err, sizeof(h), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (p->h_sweep_err && *static_cast<volatile uint32_t*>(p->h_sweep_err) != 0u) h = 1u;
   if (h) {
     HIP_TRY(hipMemsetAsync(err, 0, sizeof(uint32_t), st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (p->h_sweep_err) *static_cast<volatile uint32_t*>(p->h_sweep_err) = 0u;
   }
   *status = int(h);
   return DG_OK;

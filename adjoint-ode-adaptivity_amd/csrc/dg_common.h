@@ -13,6 +13,7 @@
 #include <new>
 #include <string>
 #include <tuple>
+#include <vector>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -455,6 +456,20 @@ struct dg_plan {
   size_t sweep_bytes = 0;
   size_t sweep_sync = 0;  // bytes of its control region (zeroed, then kept by epochs)
   int64_t sweep_items = -1;  // work items of the last dataflow launch on that region
+  // the shape the control words were last zeroed for (items, waves, steps per block, nsteps,
+  // adjoint tiles): the take counter counts launches modulo the items and the fused refine's
+  // arrival counter modulo the last block's tiles, so any change of these zeroes them
+  uint64_t sweep_sig = 0;
+  // scratch regions a grown scratch replaced: kept until the plan is destroyed, because a HIP
+  // graph captured earlier still holds their addresses in its kernel arguments
+  std::vector<void*> sweep_retired;
+  // watchdog: polls before a waiting work item gives up (0: the default, ~2^20; tests set 1)
+  int sweep_spin_limit = 0;
+  // the watchdog's host-visible flag (mapped page-locked word; the device alias is what the
+  // kernel writes): set by a work item that gave up, read without a sync by the next sweep
+  // call (which then fails) and cleared by dg_sweep_status
+  uint32_t* h_sweep_err = nullptr;
+  uint32_t* d_sweep_err = nullptr;
   int rec_sweep = 1;
   uint64_t* sweep_trace = nullptr;  // dg_plan_sweep_trace: per-item timestamps (profiling)
   int cu_count = 0;  // compute units of the plan's device (the dataflow grid)
@@ -603,6 +618,8 @@ struct SweepBufs {
   int64_t* am_nf;
   double* am_pv;    // partial winners, one per last-block tile
   int64_t* am_pi;
+  uint32_t* err_host;  // nullable: the plan's host-visible watchdog flag (d_sweep_err)
+  int32_t spin_limit;  // 0: the default
 };
 int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps);
 int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa);

@@ -30,9 +30,12 @@
 //   workgroup reads can change after it was read.
 // Epochs: a 64-bit take counter that only grows numbers the launches (value / items) and the
 // items (value % items); the flags hold the launch's epoch, so no memset precedes a launch
-// of the same shape and HIP-graph replays work.  Every poll is bounded: a producer that never finishes (a bug) sets
-// the error word after ~2^20 polls and every waiter gives up, so the launch always ends;
-// dg_sweep_status() reports it.
+// of the same shape and HIP-graph replays work.  Every poll is bounded: a producer that never
+// finishes (a bug) sets the error word after ~2^20 polls and every waiter gives up, so the
+// launch always ends.  A work item that gave up writes NaN over what it publishes, so the
+// indicator and the fused refine value turn non-finite; the error is also raised in mapped
+// host memory, which makes the plan's next sweep call fail, and dg_sweep_status() reports
+// and clears it.
 // The results are bit-identical to the launch-per-block pair with the same steps per block
 // (same tile arithmetic; the indicator's block partials are added in launch order).
 #include "dg_rec_tiles.h"
@@ -65,6 +68,7 @@ template <int NP, int MSF> struct SweepArgs {
   int64_t* am_nf;
   double* am_pv;                   // per last-block tile: its (|eta|, element) winner
   int64_t* am_pi;
+  uint32_t* err_host;              // nullable: mapped host word, raised with the error word
   int32_t nbF, nbA, nTF, nTA;
   int32_t nsteps;
   int32_t mode;                    // kEta* bits (0: no indicator)
@@ -78,9 +82,11 @@ __device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave 0: wait until flags[0..nd) all hold `epoch` (one lane per flag, nd <= 64).
-__device__ __forceinline__ void sweep_wait(const uint32_t* flags, int nd, uint32_t epoch,
-                                           uint32_t* sync, int limit) {
+// Wave 0: wait until flags[0..nd) all hold `epoch` (one lane per flag, nd <= 64).  Returns
+// true (wave-uniform) if it gave up: after `limit` polls (a producer that never finishes; the
+// sweep's error word and the host-visible flag are raised) or on seeing the error word.
+__device__ __forceinline__ bool sweep_wait(const uint32_t* flags, int nd, uint32_t epoch,
+                                           uint32_t* sync, uint32_t* err_host, int limit) {
   const int l = threadIdx.x & 63;
   bool ok = l >= nd;
   if (!ok) ok = ld_agent(flags + l) == epoch;
@@ -88,12 +94,28 @@ __device__ __forceinline__ void sweep_wait(const uint32_t* flags, int nd, uint32
   while (!__all(ok)) {
     __builtin_amdgcn_s_sleep(2);
     if (!ok) ok = ld_agent(flags + l) == epoch;
-    if (++spins >= limit) {  // a producer that never finishes: flag the sweep, give up
-      if (l == 0) st_agent(sync + kSyncErr, 1u);
-      break;
+    if (++spins >= limit) {
+      if (l == 0) {
+        st_agent(sync + kSyncErr, 1u);
+        if (err_host)
+          __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      return true;
     }
-    if ((spins & 255) == 0 && ld_agent(sync + kSyncErr) != 0u) break;  // someone gave up
+    if ((spins & 255) == 0 && ld_agent(sync + kSyncErr) != 0u) return true;  // someone gave up
   }
+  return false;
+}
+
+// A work item that gave up computed on inputs that may not have been ready: it overwrites
+// what it publishes with NaN (write-through, like the outputs), so every consumer, the
+// indicator and the fused refine decision turn non-finite and the callers' checks fire.
+template <int LB>
+__device__ __forceinline__ void poison_run(double* __restrict__ g, int64_t o0, int64_t count) {
+  if (count <= 0) return;
+  const __amdgpu_buffer_rsrc_t r = wt_rsrc(g + o0);
+  const double q = __builtin_nan("");
+  for (int64_t v = threadIdx.x; v < count; v += LB) wt_st8(r, uint32_t(v) * 8u, q);
 }
 
 // Winner of (v, i) over the NW-wave workgroup under am_better; valid in thread 0.  sv / si:
@@ -139,7 +161,7 @@ __global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
   constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
   constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MSF * 6 + 1];
-  __shared__ uint32_t s_item, s_epoch, s_last;
+  __shared__ uint32_t s_item, s_epoch, s_last, s_bad;
   __shared__ double s_av[NW];
   __shared__ int64_t s_ai[NW];
   uint32_t* sync = a.sync;
@@ -159,6 +181,7 @@ __global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
                                               __HIP_MEMORY_SCOPE_AGENT);
     s_epoch = uint32_t(h / uint64_t(nItems)) + 1u;
     s_item = uint32_t(h % uint64_t(nItems));
+    s_bad = 0u;
   }
   __syncthreads();
   const int64_t item = s_item;
@@ -195,7 +218,10 @@ __global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
         nd = hi - lo + 1;
       }
     }
-    if (tid < 64 && nd > 0) sweep_wait(flags + d0, nd, epoch, sync, a.spin_limit);
+    if (tid < 64 && nd > 0) {
+      const bool gave_up = sweep_wait(flags + d0, nd, epoch, sync, a.err_host, a.spin_limit);
+      if (tid == 0 && gave_up) s_bad = 1u;
+    }
     // no acquire fence: every load of handed-off bytes below is an sc1 load; this only keeps
     // the compiler from hoisting them above the poll
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -215,6 +241,11 @@ __global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
       else
         rp_step_tile<NP, UNI, NW, E, MSF, false, true>(lds, j, a.U[blk], a.rec, a.U[blk + 1],
                                                        a.scale, a.c, kb, n0, jend);
+      if (s_bad) {  // after the body's final barrier: its stores are issued, ours follow
+        const int64_t o0 = int64_t(j) * TEF * NP, nd = ktot * NP;
+        poison_run<64 * NW>(a.U[blk + 1], o0, (nd - o0) < int64_t(TEF) * NP ? nd - o0
+                                                                            : int64_t(TEF) * NP);
+      }
     } else {
       const int64_t e0 = int64_t(j) * TEA - HA;
       const bool lastb = blk == a.nbA - 1;
@@ -235,6 +266,14 @@ __global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
       else
         rp_adj_tile<NP, UNI, NW, E, MSA, false, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
                                                       a.scale, a.c, n0);
+      if (s_bad) {
+        const int64_t o0 = int64_t(j) * TEA, nd = ktot * NP;
+        const int64_t ne = (ktot - o0) < TEA ? ktot - o0 : int64_t(TEA);
+        poison_run<64 * NW>(a.W[blk + 1], o0 * NP, (nd - o0 * NP) < int64_t(TEA) * NP
+                                                       ? nd - o0 * NP : int64_t(TEA) * NP);
+        if (a.mode) poison_run<64 * NW>(es.part_out ? es.part_out : a.eta, o0, ne);
+        es.bv = __builtin_nan("");
+      }
       if (es.argmax) {  // the tile's winner, a hand-off to the last arriving tile
         wg_argmax<NW>(es.bv, es.bi, s_av, s_ai);
         if (tid == 0) {
@@ -272,6 +311,7 @@ __global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
         }
         wg_argmax<NW>(v, i, s_av, s_ai);
         if (tid == 0) {
+          if (ld_agent(sync + kSyncErr) != 0u) v = __builtin_nan("");  // a work item gave up
           a.am_idx[0] = i;
           if (a.am_val) a.am_val[0] = v;
           if (a.am_nf && !isfinite(v)) a.am_nf[0] += 1;
@@ -325,7 +365,8 @@ int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int 
   a.nTA = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSA>::A));
   a.nsteps = nsteps;
   a.mode = mode;
-  a.spin_limit = kSweepSpinLimit;
+  a.err_host = b.err_host;
+  a.spin_limit = b.spin_limit > 0 ? b.spin_limit : kSweepSpinLimit;
   const int64_t items = int64_t(nbF) * a.nTF + int64_t(nbA) * a.nTA;
   hipLaunchKernelGGL((k_sweep_rp<NP, UNI, NW, MSF, MSA>), dim3(unsigned(items)), dim3(64 * NW), 0,
                      st, a);

@@ -296,8 +296,14 @@ def gather_indicator(partial, n_total, reducer, group=None):
   else:
     # one slice: its sum is itself
     total = partial
-  # dividing by 1 is exact (bit-identical shortcut)
-  mean = total / float(n_total) if n_total != 1 else total
+  # dividing by 1 is exact (bit-identical shortcut).  The divisor is a 0-dim tensor on the
+  # indicator's device: with a Python float PyTorch's CUDA division multiplies by the
+  # reciprocal (a * (1/b), one ulp off a / b for b = 3, 6, 12, ...), while dg_slice_candidate
+  # (refine_decision at W > 1) divides; a tensor divisor keeps true division on both paths.
+  if n_total != 1:
+    mean = torch.div(total, torch.tensor(float(n_total), dtype=total.dtype, device=total.device))
+  else:
+    mean = total
   return mean, reducer.argmax(mean)
 
 

@@ -116,6 +116,9 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             workgroups of 256*value lanes, one element per lane (default 2)
  *   DG_TUNE_P_STEPS_PER_LAUNCH its steps per launch: 1, 2, 4 (default) or 8 (8 needs tile
  *                             width 2, else 4); a sweep is chunked by halving
+ *   DG_TUNE_SWEEP_SPIN_LIMIT  diagnostics/tests: polls a dataflow work item makes before it
+ *                             gives up waiting for a producer (0: the default, ~2^20; 1 makes
+ *                             the watchdog fire on any multi-block sweep)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
  * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
  * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH. */
@@ -123,7 +126,8 @@ enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER =
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
        DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10,
-       DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12 };
+       DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12,
+       DG_TUNE_SWEEP_SPIN_LIMIT = 13 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
@@ -278,7 +282,12 @@ int dg_plan_query_sweep(const dg_plan* plan, int nsteps, int64_t out[4]);
 /* dg_plan_query_sweep plus out[4] = workgroup waves, out[5] = elements per tile. */
 int dg_plan_query_sweep_ex(const dg_plan* plan, int nsteps, int64_t out[6]);
 /* Synchronises `stream`; *status = 0, or 1 if a dataflow sweep since the last call gave up
- * waiting for a producer (a bug: its outputs are garbage; the launch still ended). */
+ * waiting for a producer (a bug, or DG_TUNE_SWEEP_SPIN_LIMIT), and clears the flag.  A work
+ * item that gives up still computes, so the launch ends, but it writes NaN over its outputs
+ * (states, indicator rows, its refine candidate): eta and the fused refine value are then not
+ * finite and nonfinite_count counts it.  The flag is also raised in mapped host memory: every
+ * later dg_lserk4_sweep_rec / dg_lserk4_sweep_refine call of the plan returns DG_ERR_HIP
+ * (without a device sync) until dg_sweep_status clears it. */
 int dg_sweep_status(dg_plan* plan, int* status, void* stream);
 /* Profiling: with trace non-null (device, 4 uint64 per work item, dg_plan_query_sweep's
  * out[3] items), every later dataflow sweep of the plan records per item the wall-clock

@@ -51,7 +51,11 @@ def test_bench_single_rank_line(gpu, dataflow):
   for key in keys:
     assert 0 < fp[key] <= 1, key
   assert fp["adj_issued_frac"] >= fp["adj_frac"] and fp["fwd_halo_factor"] > 1
-  assert out["indicator"] == "jump" and "resolved" in out["indicator_resolved"]
+  assert out["indicator"] == "jump"
+  d = out["refine_decision"]
+  assert d["index"] == out["refine_index"] and d["top1"] >= d["top2"] >= 0
+  assert d["rounding_floor"] >= 0 and isinstance(d["decided"], bool)
+  assert d["decided"] == (d["margin"] > d["rounding_floor"] and d["index_alt"] == d["index"])
   assert out["library"]["path"].endswith("libdgadv.so") and not out["library"]["override"]
 
 

@@ -174,3 +174,79 @@ def test_device_reducer_candidates_pick_the_full_argmax(pkg, gpu, kind, n_total)
   assert int(red.nonfinite[0]) == (1 if kind == "nan" else 0)
   if kind == "tie":
     assert want == 2500
+
+
+@pytest.mark.parametrize("use_abs", [0, 1])
+def test_argmax_winner_past_the_first_grid_stride_pass(pkg, gpu, use_abs):
+  """k_argmax_partial's threads each see several elements (grid-stride loop): winners placed
+  in the last pass, among all-negative values (use_abs = 0: no |.| to lift them above the
+  start value), with a -inf and a tie, are found with numpy's index and value.  Guards the
+  loop form ROCm 7.2 miscompiled in k_slice_partial (profiles/probes/argmax_phi_copy.hip)."""
+  import torch
+  n = 300007  # ~ 293 partial blocks of 256 threads: 4 passes per thread
+  mesh = pkg.BaseGalerkin1D(n=2, k=n)
+  op = pkg.operators.DGAdvection1D(mesh)
+  rng = np.random.default_rng(3)
+  x = -1.0 - rng.random(n)  # all negative
+  if not use_abs:
+    x[17] = -np.inf  # the weakest value there is: it must still lose to every other
+  for where in (n - 1, n - 300, 250000, 1024 * 7 + 5):
+    y = x.copy()
+    y[where] = -50.0 if use_abs else -0.5  # the maximum of |y| / of y
+    y[where + 1 if where + 1 < n else where - 1] = y[where]  # a tie: the lower index wins
+    want = int(np.argmax(np.abs(y) if use_abs else y))
+    assert want <= where
+    t = torch.tensor(y, device=gpu)
+    idx = torch.zeros(1, dtype=torch.int64, device=gpu)
+    val = torch.zeros(1, dtype=torch.float64, device=gpu)
+    op.argmax_ex(t, idx, val, use_abs=bool(use_abs))
+    torch.cuda.synchronize()
+    assert int(idx.item()) == want, (where, int(idx.item()), want)
+    ref = abs(y[want]) if use_abs else y[want]
+    assert float(val.item()) == ref
+
+
+@pytest.mark.parametrize("rows,divisor", [(1, 3.0), (4, 3.0), (4, 6.0), (2, 1.0)])
+def test_slice_candidate_winner_past_the_first_pass(pkg, gpu, rows, divisor):
+  """dg_slice_candidate (rank-order row sum, division, argmax of |m|) with the winner in the
+  last grid-stride pass and divisors whose reciprocal is inexact: index and value bits of
+  numpy's argmax of |sum / divisor| (true division)."""
+  import torch
+  n, ld = 200003, 200011
+  mesh = pkg.BaseGalerkin1D(n=2, k=n)
+  red = pkg.ensemble.DeviceReducer(pkg.operators.DGAdvection1D(mesh))
+  rng = np.random.default_rng(rows * 7 + int(divisor))
+  x = rng.random((rows, ld))
+  x[:, n - 2] = 5.0  # beyond every thread's first pass
+  m = oadj.sum_rows(x[:, :n]) / divisor
+  want = int(np.argmax(np.abs(m)))
+  assert want == n - 2
+  c = red.candidate(torch.tensor(x, device=gpu), n, divisor, 100)
+  torch.cuda.synchronize()
+  c = host(c)
+  assert int(c[1]) == want + 100
+  assert c[0:1].view(np.float64)[0] == np.abs(m[want])
+
+
+@pytest.mark.parametrize("n_total", [3, 6, 12])
+def test_gather_indicator_divides_like_the_candidate_kernel(pkg, gpu, n_total):
+  """refine_decision (dg_slice_candidate: true division on the device) and gather_indicator
+  (torch division of the summed indicator) give the same index and value bit for bit on the
+  GPU for IC counts whose reciprocal is inexact (a Python-float divisor would make PyTorch
+  multiply by the reciprocal, one ulp away), and the mean equals numpy's total / n."""
+  import torch
+  K = 40009
+  mesh = pkg.BaseGalerkin1D(n=2, k=K)
+  red = pkg.ensemble.DeviceReducer(pkg.operators.DGAdvection1D(mesh))
+  rng = np.random.default_rng(n_total)
+  total = rng.random(K) * 10.0 ** rng.integers(-3, 3, K)
+  t = torch.tensor(total, device=gpu)
+  mean, idx = pkg.ensemble.gather_indicator(t, n_total, red)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(host(mean), total / float(n_total))
+  i_g, v_g = int(idx.item()), host(red.value)[0]
+  c = red.candidate(t.view(1, K), K, float(n_total), 0)
+  red.finish(c.view(1, 2))
+  torch.cuda.synchronize()
+  assert int(red.idx.item()) == i_g
+  assert host(red.value)[0] == v_g

@@ -130,3 +130,138 @@ def test_full_size_config2_record_default(pkg, gpu, N):
   a = np.sort(np.abs(eta_ref))
   if a[-1] - a[-2] > RTOL * a[-1]:
     assert op.argmax(eta) == int(np.argmax(np.abs(eta_ref)))
+
+
+def _oracle_sweep(u0, N, S, dt, nsteps, inflow="a"):
+  """The oracle's forward march and adjoint sweep for J = |u^N|^2/2 (w^N = u^N):
+  (u^N, w^0, |eta|) on (Np, K) arrays (utils/One_code.mlx:106-140,
+  python/Main_finite_difference.py:54-94 patterns)."""
+  ref, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, A, S, inflow=inflow)
+  w_ref, eta_ref, _ = oadj.adjoint_sweep(ref[-1], ref, times, dt, A, S, inflow=inflow)
+  return ref[-1], w_ref, np.abs(eta_ref)
+
+
+def _margin(a_eta):
+  """Top-1 / top-2 of |eta| and their gap, relative to the top."""
+  a = np.sort(a_eta)
+  return {"top1": float(a[-1]), "top2": float(a[-2]),
+          "margin_rel": float((a[-1] - a[-2]) / a[-1]) if a[-1] > 0 else 0.0}
+
+
+@pytest.mark.parametrize("N", [4, 6])
+def test_full_size_dataflow_sweep_refine(pkg, gpu, N):
+  """THE TIMED PATH at config 2's size: dg_lserk4_sweep_refine as the bench runs it -- ONE
+  k_sweep_rp dataflow launch (default shape: a 20-step forward block, 10 + 10 adjoint blocks,
+  1024-element tiles; at K = 2^20 about 3,500 work items with in-launch hand-offs between
+  tiles and the refine argmax reduced across ~1,100 tiles inside the launch) -- against the
+  oracle's own forward and adjoint at 1e-10 of max|oracle|: u^N, w^0 and |eta|, and the refine
+  index equal to numpy's argmax of the oracle's |eta| (its top-2 margin is far above the bar
+  on this IC).  IC: a sine plus seeded per-node noise, whose O(0.1) jumps keep the indicator
+  as well conditioned as the states (the plain sine's is rounding noise at h = 2^-20, see
+  test_full_size_bench_workload)."""
+  import torch
+  K, nsteps = 1 << 20, 20
+  _, v_x, _, _ = setup1d.mesh_gen1d(0.0, 1.0, K)
+  S = setup1d.startup1d(N, v_x, metric="element")
+  op = pkg.operators.DGAdvection1D(pkg.BaseGalerkin1D(n=N, v_x=v_x))
+  on, fsteps, asteps, items = op.query_sweep(nsteps)
+  assert on and (fsteps, asteps) == (20, 10) and items > 3000, (on, fsteps, asteps, items)
+  u0 = np.sin(2 * np.pi * S["x"]) + 0.1 * np.random.default_rng(10 + N).standard_normal(S["x"].shape)
+  dt = oadv.bench_dt(S)
+  uN_ref, w_ref, eta_ref = _oracle_sweep(u0, N, S, dt, nsteps)
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  rec, w, uN = op.new_jumps(nsteps), op.new_field(), op.new_field()
+  eta = torch.full((K,), float("nan"), dtype=torch.float64, device=gpu)
+  res = torch.zeros(3, dtype=torch.int64, device=gpu)
+  op.sweep_refine(u, rec, w, 0.0, dt, nsteps, eta, res[0:1], res[1:2].view(torch.float64),
+                  res[2:3], uN=uN)
+  torch.cuda.synchronize()
+  assert op.sweep_status() == 0
+  assert rel_err(setup1d.from_elem_major(host(uN), N + 1), uN_ref) <= RTOL
+  assert rel_err(setup1d.from_elem_major(host(w), N + 1), w_ref) <= RTOL
+  assert rel_err(host(eta), eta_ref) <= RTOL
+  m = _margin(eta_ref)
+  assert m["margin_rel"] > 1e3 * RTOL, m  # the decision is not a rounding call on this IC
+  want = int(np.argmax(eta_ref))
+  assert int(host(res)[0]) == want
+  assert host(res[1:2].view(torch.float64))[0] == host(eta)[want] and int(host(res)[2]) == 0
+
+
+def test_full_size_bench_workload(pkg, gpu):
+  """The bench's own workload (config 2: u0 = sin(2 pi x), inflow -sin(a t), K = 2^20, N = 4,
+  the dataflow sweep + fused refine) against the oracle: u^N and w^0 within 1e-10.  Its
+  indicator is rounding noise (h = 2^-20: the smooth sine's interelement jumps, O(h^5), are
+  below fp64 resolution of the states), so |eta| is compared against the rounding floor
+  instead: the GPU-vs-oracle difference must stay below 5 % of max|eta|, the same order as the
+  spread the oracle's own |eta| shows between two fp64 evaluation orders would give.  The
+  refine index is asserted only when the oracle's top-2 margin exceeds that difference; the
+  margins are written to gpurun_out/bench_workload_margin.json for profiles/r04/."""
+  import json
+  import os
+  import torch
+  N, K, nsteps = 4, 1 << 20, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K, domain=[0.0, 1.0])  # the bench's mesh and dt
+  S = setup1d.startup1d(N, np.asarray(mesh.v_x), metric="element")
+  op = pkg.operators.DGAdvection1D(mesh)
+  dt = mesh.cfl_dt()
+  u = op.new_field()
+  op.init_sine(np.array([1.0]), np.array([1.0]), np.array([0.0]), out=u)  # bench rank 0's IC
+  u0 = setup1d.from_elem_major(host(u), N + 1)
+  uN_ref, w_ref, eta_ref = _oracle_sweep(u0, N, S, dt, nsteps)
+  rec, w, uN = op.new_jumps(nsteps), op.new_field(), op.new_field()
+  eta = torch.empty(K, dtype=torch.float64, device=gpu)
+  res = torch.zeros(3, dtype=torch.int64, device=gpu)
+  op.sweep_refine(u, rec, w, 0.0, dt, nsteps, eta, res[0:1], res[1:2].view(torch.float64),
+                  res[2:3], uN=uN)
+  torch.cuda.synchronize()
+  assert op.sweep_status() == 0
+  assert rel_err(setup1d.from_elem_major(host(uN), N + 1), uN_ref) <= RTOL
+  assert rel_err(setup1d.from_elem_major(host(w), N + 1), w_ref) <= RTOL
+  e = host(eta)
+  diff = float(np.max(np.abs(e - eta_ref)))
+  m_ref, m_gpu = _margin(eta_ref), _margin(e)
+  rec_m = {"what": "bench workload (config 2, u0 = sin 2 pi x, K = 2^20, N = 4): oracle vs "
+                   "the GPU's dataflow sweep",
+           "oracle": m_ref, "gpu": m_gpu, "max_abs_eta_diff": diff,
+           "diff_over_top1": diff / m_ref["top1"],
+           "oracle_index": int(np.argmax(eta_ref)), "gpu_index": int(host(res)[0]),
+           "decided_by_oracle_margin": bool(m_ref["top1"] - m_ref["top2"] > 2 * diff)}
+  print("BENCH_WORKLOAD_MARGIN", json.dumps(rec_m))
+  os.makedirs("gpurun_out", exist_ok=True)
+  with open(os.path.join("gpurun_out", "bench_workload_margin.json"), "w") as f:
+    json.dump(rec_m, f, indent=1)
+  assert diff <= 0.05 * m_ref["top1"], rec_m
+  assert int(host(res)[0]) == int(np.argmax(e))
+  if rec_m["decided_by_oracle_margin"]:
+    assert rec_m["gpu_index"] == rec_m["oracle_index"], rec_m
+
+
+def test_full_size_dataflow_config4_shape(pkg, gpu):
+  """Config 4's batched shape on the dataflow launch: 1024 trajectories x K = 65,536 (67 M
+  elements: the forward runs 10 + 10 blocks), noisy sine ICs, |eta| per trajectory.  Sampled
+  rows (the first, a middle and the last trajectory, whose tiles hold trajectory edges) are
+  compared with the oracle run on that IC alone at 1e-10: u^N, w^0 and |eta|."""
+  import torch
+  K, n_ics, nsteps, N = 65536, 1024, 20, 4
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh, batch=n_ics)
+  on, fsteps, asteps, _ = op.query_sweep(nsteps)
+  assert on and (fsteps, asteps) == (10, 10)
+  amp, freq, phase = pkg.ensemble.ic_params(range(n_ics))
+  u0 = op.init_sine(amp, freq, phase)
+  gen = torch.Generator(device=gpu).manual_seed(4)
+  u0 += 0.1 * torch.randn(u0.shape, dtype=u0.dtype, device=gpu, generator=gen)
+  dt = mesh.cfl_dt()
+  rec, w, uN = op.new_jumps(nsteps), op.new_field(), op.new_field()
+  eta = torch.full((op.ktot,), float("nan"), dtype=torch.float64, device=gpu)
+  op.sweep_rec(u0, rec, w, 0.0, dt, nsteps, uN=uN, eta=eta, eta_assign=True, eta_abs=True)
+  torch.cuda.synchronize()
+  assert op.sweep_status() == 0
+  S = setup1d.uniform_setup(N, K, metric="element")
+  fs = K * (N + 1)
+  for j in (0, 511, 1023):
+    u0j = setup1d.from_elem_major(host(u0[j * fs:(j + 1) * fs]), N + 1)
+    uN_ref, w_ref, eta_ref = _oracle_sweep(u0j, N, S, dt, nsteps)
+    assert rel_err(setup1d.from_elem_major(host(uN[j * fs:(j + 1) * fs]), N + 1), uN_ref) <= RTOL, j
+    assert rel_err(setup1d.from_elem_major(host(w[j * fs:(j + 1) * fs]), N + 1), w_ref) <= RTOL, j
+    assert rel_err(host(eta[j * K:(j + 1) * K]), eta_ref) <= RTOL, j

@@ -12,8 +12,9 @@ Bars:
     hand-offs, cdna_hip_programming.md §6 Guideline 16 pitfall 3) too;
   * no launch gives up waiting for a producer (dg_sweep_status);
   * shapes the dataflow launch does not cover fall back to the two launch chains (query).
-The oracle comparison of this path at full size is tests/test_gpu_full_size.py (the bench's
-EnsembleSweep runs it).
+The oracle comparison of this path at full size (the bench's timed launch, K = 2^20 at N = 4
+and 6, and config 4's batched shape) is tests/test_gpu_full_size.py::test_full_size_dataflow_*;
+the watchdog's give-up path is test_watchdog_gives_up_loudly below.
 """
 import numpy as np
 import pytest
@@ -300,3 +301,104 @@ def test_sweep_refine_into_pinned_host_memory(pkg, gpu):
     torch.cuda.synchronize()
     assert host_buf.tolist() == host(dev)[:2].tolist()
   assert int(nf.item()) == 0
+
+
+def test_watchdog_gives_up_loudly(pkg, gpu):
+  """A work item that gives up waiting for its producers (here forced: the test-only tune key
+  DG_TUNE_SWEEP_SPIN_LIMIT = 1 on a multi-block sweep) poisons what it publishes: the fused
+  refine value is NaN and the non-finite count fires, eta holds NaN, the plan's next sweep
+  call raises until sweep_status() reports and clears the flag, and a normal launch after
+  that gives the launch chains' bits again."""
+  import torch
+  N, K, nsteps = 4, 1 << 18, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  assert op.query_sweep(nsteps)[:3] == (True, 20, 10)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 5, 1)
+  ref = run_sweep(op, u0, dt, nsteps, False)
+  op.tune(rec_sweep=1)
+  _lib = pkg._lib
+  _lib.check(op._lib.dg_plan_tune(op._plan, _lib.DG_TUNE_SWEEP_SPIN_LIMIT, 1), "dg_plan_tune")
+  rec, w = op.new_jumps(nsteps), op.new_field()
+  eta = torch.zeros(op.ktot, dtype=torch.float64, device=gpu)
+  got = torch.zeros(3, dtype=torch.int64, device=gpu)
+  op.sweep_refine(u0, rec, w, 0.0, dt, nsteps, eta, got[0:1], got[1:2].view(torch.float64),
+                  got[2:3])
+  torch.cuda.synchronize()
+  assert np.isnan(host(got[1:2].view(torch.float64))[0]), "the fused value must be NaN"
+  assert int(host(got)[2]) == 1
+  assert np.isnan(host(eta)).any()
+  with pytest.raises(pkg._lib.DGLibraryError, match="gave up"):
+    op.sweep_refine(u0, rec, w, 0.0, dt, nsteps, eta, got[0:1], got[1:2].view(torch.float64),
+                    got[2:3])
+  assert op.sweep_status() == 1
+  assert op.sweep_status() == 0  # cleared
+  _lib.check(op._lib.dg_plan_tune(op._plan, _lib.DG_TUNE_SWEEP_SPIN_LIMIT, 0), "dg_plan_tune")
+  assert_same(run_sweep(op, u0, dt, nsteps, True), ref, "after the watchdog fired")
+
+
+def test_grown_scratch_keeps_captured_graph_valid(pkg, gpu):
+  """A graph captured around sweep_rec keeps the scratch addresses in its kernel arguments;
+  a later call that needs more scratch (sweep_refine's argmax slots, a longer sweep) must not
+  free them: the replay still gives the same bits."""
+  import torch
+  N, K, nsteps = 4, 30000, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 8, 1)
+  ref = run_sweep(op, u0, dt, nsteps, False)
+  op.tune(rec_sweep=1)
+  rec, uN, w = op.new_jumps(nsteps), op.new_field(), op.new_field()
+  eta = torch.zeros(op.ktot, dtype=torch.float64, device=gpu)
+
+  def sweep():
+    op.sweep_rec(u0, rec, w, 0.0, dt, nsteps, uN=uN, eta=eta, eta_assign=True)
+
+  sweep()
+  torch.cuda.synchronize()
+  g = torch.cuda.CUDAGraph()
+  with torch.cuda.graph(g):
+    sweep()
+  # grow the scratch: a 40-step sweep, then the fused refine decision
+  run_sweep(op, u0, dt, 40, True)
+  got = torch.zeros(3, dtype=torch.int64, device=gpu)
+  rec40, w40 = op.new_jumps(40), op.new_field()
+  e40 = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+  op.sweep_refine(u0, rec40, w40, 0.0, dt, 40, e40, got[0:1])
+  torch.cuda.synchronize()
+  for _ in range(2):
+    w.zero_()
+    eta.zero_()
+    uN.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert_same((host(uN), host(rec), host(w), host(eta)), ref, "graph replay after growth")
+  assert op.sweep_status() == 0
+
+
+def test_alternating_shapes_keep_refine_aligned(pkg, gpu):
+  """Launch shapes alternating on one plan (adjoint blocks of 10 and 5 steps: different
+  adjoint tile counts) re-zero the control words on every change, so the fused refine's
+  arrival counter and the take counter stay aligned: each decision equals dg_argmax_ex."""
+  import torch
+  N, K, nsteps = 4, 50000, 20
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 12, 1)
+  rec, w = op.new_jumps(nsteps), op.new_field()
+  eta = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+  got = torch.zeros(3, dtype=torch.int64, device=gpu)
+  ref = torch.zeros(3, dtype=torch.int64, device=gpu)
+  for rep in range(3):
+    for asteps in (10, 5):
+      op.tune(rec_steps_per_launch=asteps, rec_fwd_steps_per_launch=20, rec_sweep=1)
+      assert op.query_sweep(nsteps)[:3] == (True, 20, asteps)
+      op.sweep_refine(u0, rec, w, 0.0, dt, nsteps, eta, got[0:1],
+                      got[1:2].view(torch.float64), got[2:3])
+      op.argmax_ex(eta, ref[0:1], ref[1:2].view(torch.float64), ref[2:3], use_abs=True)
+      torch.cuda.synchronize()
+      assert host(got)[:2].tolist() == host(ref)[:2].tolist(), (rep, asteps)
+  assert op.sweep_status() == 0
