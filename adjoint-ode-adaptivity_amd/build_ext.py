@@ -27,11 +27,16 @@ def hipcc():
   raise RuntimeError("hipcc not found (ROCm is required to build the HIP extension)")
 
 
-def build(force=False, verbose=True, extra_flags=(), out=None):
+def build(force=False, verbose=True, extra_flags=(), out=None, srcdir=None):
   """Build lib/libdgadv.so; `out` + `extra_flags` build an experiment variant elsewhere
-  (its own object directory; the product library is untouched)."""
+  (its own object directory; the product library is untouched); `srcdir`: a patched copy of
+  csrc/ for such a variant (A/B runs)."""
   OUT_ = OUT if out is None else os.path.abspath(out)
-  deps = SRCS + HEADERS + [os.path.join(INCLUDE, "dg_advec.h")]
+  srcs, headers = SRCS, HEADERS
+  if srcdir is not None:
+    srcs = [os.path.join(srcdir, os.path.basename(f)) for f in SRCS]
+    headers = [os.path.join(srcdir, os.path.basename(f)) for f in HEADERS]
+  deps = srcs + headers + [os.path.join(INCLUDE, "dg_advec.h")]
   if (not force and os.path.exists(OUT_)
       and os.path.getmtime(OUT_) >= max(os.path.getmtime(d) for d in deps)):
     if verbose:
@@ -43,8 +48,8 @@ def build(force=False, verbose=True, extra_flags=(), out=None):
   os.makedirs(objdir, exist_ok=True)
   flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-I", INCLUDE, *extra_flags]
   procs, objs = [], []
-  shared = max(os.path.getmtime(d) for d in deps[len(SRCS):])
-  for src in SRCS:
+  shared = max(os.path.getmtime(d) for d in deps[len(srcs):])
+  for src in srcs:
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
     objs.append(obj)
     if (not force and os.path.exists(obj)
@@ -73,5 +78,6 @@ if __name__ == "__main__":
   ap.add_argument("--force", action="store_true")
   ap.add_argument("--out", default=None, help="variant library path (experiments)")
   ap.add_argument("-D", action="append", default=[], help="extra -D defines")
+  ap.add_argument("--srcdir", default=None, help="patched csrc/ copy for a variant")
   a = ap.parse_args()
-  build(force=a.force, out=a.out, extra_flags=tuple("-D" + d for d in a.D))
+  build(force=a.force, out=a.out, extra_flags=tuple("-D" + d for d in a.D), srcdir=a.srcdir)

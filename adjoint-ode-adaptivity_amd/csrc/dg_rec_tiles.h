@@ -663,7 +663,31 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
       __builtin_amdgcn_sched_barrier(0);
       // the transposed volume term, before the barrier: a = c w + Qoe^T qo (even), c w +
       // Qeo^T qe (odd); level 0 starts from the bare products
+      // odd outputs first (they read the even inputs, which then die), then the even ones
+      // (reading the odd inputs): fewer values live at once than one loop over both
       double ae[E][NE], ao[E][NO];
+#pragma unroll
+      for (int m = 0; m < E; ++m) {
+#pragma unroll
+        for (int j = 0; j < NO; ++j) {
+          double t;
+          int k0 = 0;
+          if (l >= 3) {
+            t = wo[m][j];
+          } else if (l >= 1) {
+            t = (l == 1 ? b3 : b2) * wo[m][j];
+          } else {
+            t = c.op.Qeo[j] * qe[m][0];
+            k0 = 1;
+          }
+#pragma unroll
+          for (int k = k0; k < NE; ++k) t = fma(c.op.Qeo[k * NO + j], qe[m][k], t);
+          ao[m][j] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) pin(ao[m][k]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < E; ++m) {
 #pragma unroll
@@ -683,25 +707,7 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
           ae[m][j] = t;
         }
 #pragma unroll
-        for (int j = 0; j < NO; ++j) {
-          double t;
-          int k0 = 0;
-          if (l >= 3) {
-            t = wo[m][j];
-          } else if (l >= 1) {
-            t = (l == 1 ? b3 : b2) * wo[m][j];
-          } else {
-            t = c.op.Qeo[j] * qe[m][0];
-            k0 = 1;
-          }
-#pragma unroll
-          for (int k = k0; k < NE; ++k) t = fma(c.op.Qeo[k * NO + j], qe[m][k], t);
-          ao[m][j] = t;
-        }
-#pragma unroll
         for (int k = 0; k < NE; ++k) pin(ae[m][k]);
-#pragma unroll
-        for (int k = 0; k < NO; ++k) pin(ao[m][k]);
       }
       __syncthreads();
       // lane-1's last element's g1 / lane+1's first element's g0

@@ -154,8 +154,20 @@ __device__ __forceinline__ uint64_t ld8_agent(const void* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Occupancy target.  Both bodies live in one kernel, so its registers are the adjoint's
+// (82-92 VGPRs at Np = 4, 5 unconstrained: 2 eight-wave workgroups per CU).  Capped at 80
+// (6 waves per SIMD: 3 workgroups per CU, 3 x 41 KB of LDS) the allocator keeps every level
+// loop of the uniform-mesh kernels spill-free at Np <= 5; the few spills it adds sit outside
+// the loops (the edge tiles' prologue, the indicator's partial-row combine).  Np = 6 spills
+// inside a loop at 80, and the non-uniform bodies (the metric per element) spill more: they
+// keep the unconstrained count.  (Np 2, 3 fit 6 waves unconstrained.)
+template <int NP, bool UNI> struct SweepOcc {
+  static constexpr int waves_per_simd = (UNI && NP <= 5) ? 6 : 1;  // 1: no constraint
+};
+
 template <int NP, bool UNI, int NW, int MSF, int MSA>
-__global__ __launch_bounds__(64 * NW) void k_sweep_rp(SweepArgs<NP, MSF> a) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
+    SweepOcc<NP, UNI>::waves_per_simd))) void k_sweep_rp(SweepArgs<NP, MSF> a) {
   constexpr int E = 2;
   using G = RpGeo<NP, NW, E>;
   constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
