@@ -99,9 +99,13 @@ def p_flops_per_update(Np):
 def halo_factor(T, H):
   """Lanes issued per useful lane of a tile of T elements whose launch writes T - 2 H."""
   return T / float(T - 2 * H)
-PROFILE_TRAFFIC = {  # per-launch PMC traffic of the sweep kernels (profiles/r02/collect.sh)
-    "jumps": os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
-    "snapshots": os.path.join(ROOT, "profiles", "r02", "pmc_traffic_snapshots.json")}
+PROFILE_TRAFFIC = {  # per-launch PMC traffic of the sweep kernels (profiles/r04/collect.sh)
+    "jumps": os.path.join(ROOT, "profiles", "r04", "headline", "pmc_traffic.json"),
+    "snapshots": os.path.join(ROOT, "profiles", "r02", "pmc_traffic_snapshots.json"),
+    "p": os.path.join(ROOT, "profiles", "r04", "p", "pmc_traffic.json")}
+PROFILE_SQ = {  # SQ passes of the same benches: issued fp64 instructions of the dominant kernel
+    "jumps": os.path.join(ROOT, "profiles", "r04", "headline", "sq_summary.json"),
+    "p": os.path.join(ROOT, "profiles", "r04", "p", "sq_summary.json")}
 
 
 def parse(argv=None):
@@ -141,6 +145,10 @@ def parse(argv=None):
                       "error estimate (order-(N+1) adjoint x one-step residual of the prolonged "
                       "snapshots; implies --record snapshots)")
   p.add_argument("--no-cpu-baseline", action="store_true")
+  p.add_argument("--no-margin", action="store_true",
+                 help="skip the refine-decision margin check after the timed region (it re-runs "
+                      "the sweep in another block shape: profiler passes use this so that every "
+                      "dispatch they average has the timed shape)")
   p.add_argument("--cpu-steps", type=int, default=12, help="time steps of the CPU sample")
   p.add_argument("--graph", action="store_true",
                  help="replay each sweep as a captured HIP graph (measured 1-3%% slower than "
@@ -815,13 +823,15 @@ def main(argv=None):
   adj_gbs = adj_bytes / (adj_launch_us * 1e-6) / 1e9
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
-  if os.path.exists(PROFILE_TRAFFIC[args.record]) and not pmode:
+  prof_key = "p" if pmode else args.record
+  if os.path.exists(PROFILE_TRAFFIC[prof_key]):
     try:
-      with open(PROFILE_TRAFFIC[args.record]) as f:
+      with open(PROFILE_TRAFFIC[prof_key]) as f:
         tr = json.load(f)
       if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
           and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
-          and tr.get("record", "snapshots") == args.record):
+          and tr.get("record", "snapshots") == args.record
+          and tr.get("indicator", "jump") == args.indicator):
         traffic = tr.get("adj_bytes_per_launch")
         traffic_src = tr.get("source")
     except (OSError, ValueError):
@@ -868,7 +878,7 @@ def main(argv=None):
     f_fl, a_fl = fwd_fpu * Np * ktot * nsteps, adj_fpu * Np * ktot * nsteps
     adj_tf = (f_fl + a_fl) / (adj_launch_us * 1e-6) / 1e12
     halo_adj = (f_fl * halo_fwd + a_fl * halo_adj) / (f_fl + a_fl)
-  decision = refine_margin(sweep, one_step) if world == 1 else None
+  decision = refine_margin(sweep, one_step) if world == 1 and not args.no_margin else None
   out = {
       "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
       "value": value,
@@ -953,6 +963,19 @@ def main(argv=None):
   }
   if pmode:
     out["prolong_us"] = float(np.mean(prolong_us))
+    try:  # issued fp64 of k_adj_p from the SQ passes of the same bench (profiles/r04/p/)
+      with open(PROFILE_SQ["p"]) as fh:
+        sq = json.load(fh)
+      if N == 4 and K == (1 << 20) and sweep.batch == 1 and traffic is not None:
+        f = out["roofline_fp64"]
+        fl = sq["fp64_flops_issued_per_launch"]
+        f["pmc_issued_per_launch"] = fl
+        f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
+        f["pmc_issued_over_useful"] = fl / (adj_fpu * upl)
+        f["pmc_wait_any_frac"] = sq.get("wait_any_frac_of_wave_cycles")
+        f["pmc_source"] = os.path.relpath(PROFILE_SQ["p"], ROOT)
+    except (OSError, ValueError, KeyError):
+      pass
   if dataflow:
     r = out["roofline"]
     r["kernel"] = (f"k_sweep_rp<{Np},uniform,{T_pair} elements,fwd {'+'.join(map(str, fchunks))},"
@@ -972,10 +995,10 @@ def main(argv=None):
     out["stream_copy"]["fwd_frac_of_achievable"] = None
     if out.get("roofline_effective"):
       out["roofline_effective"].update({"fwd_GBs": None, "fwd_frac": None})
-    # the PMC-measured issued fp64 flops of the same launch shape (SQ pass of this bench,
-    # profiles/r03/collect_sq_sweep.sh), when N and K match
+    # the PMC-measured issued fp64 flops of the same launch shape (SQ passes of this bench,
+    # profiles/r04/collect.sh), when N and K match
     try:
-      with open(os.path.join(ROOT, "profiles", "r03", "sq", "sq_summary_k_sweep_rp.json")) as fh:
+      with open(PROFILE_SQ["jumps"]) as fh:
         sq = json.load(fh)
       if (N == 4 and K == (1 << 20) and sweep.batch == 1 and fchunks == [20]
           and chunks == [10, 10] and T_pair == 1024):
@@ -983,7 +1006,8 @@ def main(argv=None):
         f["pmc_issued_per_launch"] = fl
         f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
         f["pmc_issued_over_useful"] = fl / ((fwd_fpu + adj_fpu) * Np * ktot * nsteps)
-        f["pmc_source"] = "profiles/r03/sq/sq_summary_k_sweep_rp.json"
+        f["pmc_wait_any_frac"] = sq.get("wait_any_frac_of_wave_cycles")
+        f["pmc_source"] = os.path.relpath(PROFILE_SQ["jumps"], ROOT)
     except (OSError, ValueError, KeyError):
       pass
     out["dataflow"] = {"launches_per_sweep": 1, "blocks_fwd": fchunks, "blocks_adj": chunks,

@@ -282,3 +282,20 @@ def test_effectivity_table_on_the_gpu(pkg, gpu, N, K):
     assert abs(o[key] - ref[key]) <= 0.02, key
   for key in ("argmax_jump", "argmax_p", "argmax_gain"):
     assert o[key] == ref[key], key
+
+
+@pytest.mark.slow
+def test_full_size_p_estimate(pkg, gpu):
+  """The p-estimate at config 2's size (N = 4, K = 2^20): 4 steps of the
+  order-N forward with snapshots, then dg_lserk4_adj_p from a seeded order-(N+1) terminal
+  weight, against oracle.effectivity.p_estimate on the GPU's own snapshots -- the whole
+  mesh (the oracle's numpy operators finish in seconds at this size) -- for eta and w^0 at
+  1e-10 of max|oracle|, plus the refine index (numpy's argmax of |eta|).  The IC is a sine
+  plus per-node noise so the residual is resolved (see test_gpu_full_size.py)."""
+  out, est = run_case(pkg, gpu, 4, 1 << 20, 4, seed=21)
+  assert (est.tile_width, est.steps_per_launch) == (2, 4)  # the default launch shape
+  check(out)
+  eta, eta_ref = out[0][0], out[0][1]
+  a = np.sort(np.abs(eta_ref))
+  assert a[-1] - a[-2] > 1e3 * RTOL * a[-1]
+  assert int(np.argmax(np.abs(eta))) == int(np.argmax(np.abs(eta_ref)))
