@@ -25,6 +25,8 @@ DG_TUNE_P_TILE_WIDTH, DG_TUNE_P_STEPS_PER_LAUNCH = 9, 10
 DG_TUNE_REC_FWD_TILE_WIDTH = 11
 DG_TUNE_REC_SWEEP = 12
 DG_TUNE_SWEEP_SPIN_LIMIT = 13
+DG_TUNE_SWEEP_WAVES = 14
+DG_TUNE_SWEEP_LANE_ELEMENTS = 15
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
@@ -45,6 +47,7 @@ SIGNATURES = {
     "dg_plan_query": (_i32, [_vp, ctypes.POINTER(_i64)]),
     "dg_plan_tune": (_i32, [_vp, _i32, _i64]),
     "dg_plan_set_physics": (_i32, [_vp, _i32, _i32]),
+    "dg_plan_set_tvb": (_i32, [_vp, ctypes.c_double]),
     "dg_plan_reserve": (_i32, [_vp, _i64]),
     "dg_plan_refine": (_i32, [_vp, _vp, _vp, _vp]),
     "dg_plan_get_mesh": (_i32, [_vp, _c_dbl_p]),

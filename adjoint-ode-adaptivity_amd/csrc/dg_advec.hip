@@ -548,6 +548,7 @@ template <int NP> struct LimArgs {
   double V1[NP];     // column 2 of V
   double Dr0[NP];    // row 1 of Dr
   double rp1h[NP];   // 0.5*(r_i + 1)  (StartUp1D.m:20)
+  double tvbM;       // > 0: SlopeLimitLin's minmod is minmodB(., M, h) (dg_plan_set_tvb)
   int64_t ktot;
   int32_t K;
 };
@@ -564,6 +565,12 @@ __device__ __forceinline__ double minmod3(double a, double b, double c) {
     return s * m;
   }
   return 0.0;
+}
+
+// The TVB-modified minmod, utils/minmodB.m:6-11: the first argument unless |a| > M h^2.
+__device__ __forceinline__ double minmod3b(double a, double b, double c, double M, double h) {
+#pragma clang fp contract(off)
+  return (fabs(a) > M * (h * h)) ? minmod3(a, b, c) : a;
 }
 
 // PI1: SlopeLimit1 (utils/SlopeLimit1.m:6-22) — the same projection and SlopeLimitLin
@@ -630,7 +637,8 @@ __global__ __launch_bounds__(kBlock) void k_limit(const double* __restrict__ u,
 #pragma unroll
     for (int j = 1; j < NP; ++j) d = d + args.Dr0[j] * ul[j];
     const double ux0 = (2.0 / h) * d;
-    const double m = minmod3(ux0, (vkp1 - vk) / h, (vk - vkm1) / h);
+    const double m = args.tvbM > 0.0 ? minmod3b(ux0, (vkp1 - vk) / h, (vk - vkm1) / h, args.tvbM, h)
+                                     : minmod3(ux0, (vkp1 - vk) / h, (vk - vkm1) / h);
 #pragma unroll
     for (int i = 0; i < NP; ++i) out[i] = vk + (x[i] - x0) * m;
   }
@@ -901,6 +909,7 @@ template <int NP> LimArgs<NP> make_lim(const dg_plan* p) {
     la.Dr0[i] = p->Dr[0 * NP + i];
     la.rp1h[i] = 0.5 * (p->r[i] + 1.0);
   }
+  la.tvbM = p->tvb_M;
   la.ktot = p->ktot;
   la.K = int32_t(p->K);
   return la;
@@ -1150,14 +1159,23 @@ inline int chunk(const dg_plan* p, int left) {
 // directions (1024 or 512 elements), the record shape's 5-, 10- or 20-step (1024 only)
 // forward and 5- or 10-step adjoint launches as its blocks, nsteps a multiple of both and at
 // most sweep_max_steps() -- else false (the launch-per-block pair runs, same results).
+// With the plan's sweep_waves set (DG_TUNE_SWEEP_WAVES) the dataflow launch runs both
+// directions on tiles of 128 * sweep_waves elements, whatever the launch chains' widths: 12
+// and 16 waves take the 10- or 20-step forward and 10-step adjoint blocks (16 at Np <= 5).
 bool sweep_shape(const dg_plan* p, int nsteps, int* waves, int* msf, int* msa) {
   const int f = rec_msteps_fwd(p), a = rec_msteps(p), w = p->rec_tile_width;
-  const int nw = 4 * w;
+  const int sw = p->sweep_waves;
+  const int nw = sw ? sw : 4 * w;
   *msf = f;
   *msa = a;
   *waves = nw;
-  return p->rec_sweep && rec_pairs(p) && rec_fwd_width(p) == w && (w == 1 || w == 2) &&
-         (f == 5 || f == 10 || (f == 20 && nw == 8)) && (a == 5 || a == 10) && nsteps > 0 &&
+  const bool tiles = (sw ? ((sw == 4 || sw == 8) ||
+                            ((sw == 12 || (sw == 16 && p->NP <= 5)) && f >= 10 && a == 10))
+                         : (rec_fwd_width(p) == w && (w == 1 || w == 2))) &&
+                     (p->sweep_lane_elems == 2 || (p->NP <= 3 && (nw == 4 || nw == 8)));
+  const int T = 64 * p->sweep_lane_elems * nw;  // elements per tile
+  return p->rec_sweep && rec_pairs(p) && tiles &&
+         (f == 5 || f == 10 || (f == 20 && T >= 1024)) && (a == 5 || a == 10) && nsteps > 0 &&
          nsteps % f == 0 && nsteps % a == 0 && nsteps <= sweep_max_steps();
 }
 
@@ -1332,6 +1350,14 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     const int k = std::atoi(v);
     if (k == 0 || k == 1) p->rec_sweep = k;
   }
+  if (const char* v = std::getenv("DG_SWEEP_LANE_ELEMENTS")) {
+    const int k = std::atoi(v);
+    if (k == 2 || (k == 4 && p->NP <= 3)) p->sweep_lane_elems = k;
+  }
+  if (const char* v = std::getenv("DG_SWEEP_WAVES")) {
+    const int k = std::atoi(v);
+    if (k == 0 || k == 4 || k == 8 || k == 12 || (k == 16 && p->NP <= 5)) p->sweep_waves = k;
+  }
 
   {
     int dev = 0, cus = 0;
@@ -1454,6 +1480,16 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
         return fail(DG_ERR_ARG, "record lane elements must be 1 or 2");
       p->rec_lane_elems = int(value);
       return DG_OK;
+    case DG_TUNE_SWEEP_WAVES:
+      if (!(value == 0 || value == 4 || value == 8 || value == 12 || value == 16))
+        return fail(DG_ERR_ARG, "sweep waves: 0 (as the record tile width), 4, 8, 12 or 16");
+      p->sweep_waves = int(value);
+      return DG_OK;
+    case DG_TUNE_SWEEP_LANE_ELEMENTS:
+      if (!(value == 2 || (value == 4 && p->NP <= 3)))
+        return fail(DG_ERR_ARG, "sweep lane elements: 2, or 4 at Np <= 3");
+      p->sweep_lane_elems = int(value);
+      return DG_OK;
     case DG_TUNE_SWEEP_SPIN_LIMIT:
       if (value < 0 || value > (1 << 30)) return fail(DG_ERR_ARG, "spin limit: 0 (default) .. 2^30");
       p->sweep_spin_limit = int(value);
@@ -1482,6 +1518,13 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
     default:
       return fail(DG_ERR_ARG, "unknown tuning key");
   }
+}
+
+int dg_plan_set_tvb(dg_plan* p, double M) {
+  if (!p) return fail(DG_ERR_ARG, "null plan");
+  if (!(M >= 0.0) || !std::isfinite(M)) return fail(DG_ERR_ARG, "TVB constant M must be >= 0");
+  p->tvb_M = M;
+  return DG_OK;
 }
 
 int dg_plan_set_physics(dg_plan* p, int flux, int limiter) {
@@ -1931,7 +1974,7 @@ int dg_plan_query_sweep_ex(const dg_plan* p, int nsteps, int64_t out[6]) {
   out[2] = msa;
   out[3] = on ? sweep_items(p, waves, msf, msa, nsteps) : 0;
   out[4] = waves;
-  out[5] = 128 * int64_t(waves);
+  out[5] = 64 * int64_t(p->sweep_lane_elems) * waves;
   return DG_OK;
 }
 

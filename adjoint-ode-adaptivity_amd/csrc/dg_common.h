@@ -471,6 +471,13 @@ struct dg_plan {
   uint32_t* h_sweep_err = nullptr;
   uint32_t* d_sweep_err = nullptr;
   int rec_sweep = 1;
+  // the dataflow sweep's workgroup waves (tiles of 128 * waves elements): 0 = as the record
+  // sweeps' tile width (4 * rec_tile_width), else 4, 8, 12 or 16 (12 / 16: dataflow only, both
+  // directions on that tile, whatever the launch chains' widths; 16 at Np <= 5)
+  int sweep_waves = 0;
+  // consecutive elements per lane of the dataflow sweep's tiles: 2 (pair tiles), or 4 at
+  // Np <= 3 on 4- or 8-wave workgroups (tiles of 64 * 4 * waves elements)
+  int sweep_lane_elems = 2;
   uint64_t* sweep_trace = nullptr;  // dg_plan_sweep_trace: per-item timestamps (profiling)
   int cu_count = 0;  // compute units of the plan's device (the dataflow grid)
   int xcd_order = 1;  // XCD-aware tile order
@@ -478,6 +485,7 @@ struct dg_plan {
   // physics (dg_plan_set_physics): DG_FLUX_LINEAR / DG_FLUX_BURGERS, SlopeLimitN per stage
   int flux = 0;
   int limiter = 0;
+  double tvb_M = 0.0;  // dg_plan_set_tvb: the TVB constant of dg_slope_limit_n / _1 (0: minmod)
   bool nonlinear() const { return flux != 0 || limiter != 0; }
 };
 

@@ -190,59 +190,75 @@ __device__ __forceinline__ void rp_store(double* __restrict__ g, int64_t o0, int
   }
 }
 
-// Record row n: the lane's two left-face jumps (dg_common.h rec_ld), one 16-byte store; an
-// edge tile stores them one by one where its valid range ends between them.  `ec` (WT): the
-// tile's first in-range element, the descriptor's base.
-template <bool EDGE, bool WT>
+// Record row n: the lane's E left-face jumps jv[0..E) (dg_common.h rec_ld), one 16-byte store
+// per pair of them; an edge tile stores a pair one by one where its valid range ends between
+// them.  (A tile's valid range [H, T - H) starts and ends at even elements, so in interior
+// tiles a pair is valid or invalid as a whole.)  `ec` (WT): the tile's first in-range element,
+// the descriptor's base.
+template <int E, bool EDGE, bool WT>
 __device__ __forceinline__ void rp_rec_put(double* __restrict__ rec, int64_t n, int64_t ktot,
-                                           const Elem* El, double j0, double j1, int64_t ec) {
+                                           const Elem* El, const double* jv, int64_t ec) {
   double* row = rec + n * rec_ld(ktot);
   if constexpr (WT) {
     const __amdgpu_buffer_rsrc_t r = wt_rsrc(row + ec);
     const uint32_t o = uint32_t(El[0].e - ec) * 8u;
-    if (!EDGE || (El[0].valid && El[1].valid)) {
-      if (El[0].valid) wt_st16(r, o, double2{j0, j1});
-    } else {
-      if (El[0].valid) wt_st8(r, o, j0);
-      if (El[1].valid) wt_st8(r, o + 8u, j1);
+#pragma unroll
+    for (int q = 0; q < E; q += 2) {
+      if (!EDGE || (El[q].valid && El[q + 1].valid)) {
+        if (El[q].valid) wt_st16(r, o + 8u * q, double2{jv[q], jv[q + 1]});
+      } else {
+        if (El[q].valid) wt_st8(r, o + 8u * q, jv[q]);
+        if (El[q + 1].valid) wt_st8(r, o + 8u * (q + 1), jv[q + 1]);
+      }
     }
   } else {
-    if (!EDGE || (El[0].valid && El[1].valid)) {
-      if (El[0].valid) *reinterpret_cast<double2*>(row + El[0].e) = double2{j0, j1};
-    } else {
-      if (El[0].valid) row[El[0].e] = j0;
-      if (El[1].valid) row[El[1].e] = j1;
+#pragma unroll
+    for (int q = 0; q < E; q += 2) {
+      if (!EDGE || (El[q].valid && El[q + 1].valid)) {
+        if (El[q].valid) *reinterpret_cast<double2*>(row + El[q].e) = double2{jv[q], jv[q + 1]};
+      } else {
+        if (El[q].valid) row[El[q].e] = jv[q];
+        if (El[q + 1].valid) row[El[q + 1].e] = jv[q + 1];
+      }
     }
   }
 }
 
-// Record row n for the lane's pair starting at element ea (even): j_ea, j_ea+1 and the right
-// neighbour's j_ea+2.  Interior tiles never reach a trajectory's end, so all three are in
-// range; edge tiles read zeros outside [0, ktot).  `ec` as for rp_rec_put.
-template <bool EDGE, bool WT>
+// Record row n for the lane's E elements starting at element ea (even): j[0..E) = j_ea..
+// j_ea+E-1 and the right neighbour's j[E] = j_ea+E.  Interior tiles never reach a
+// trajectory's end, so all are in range; edge tiles read zeros outside [0, ktot).  `ec` as
+// for rp_rec_put.
+template <int E, bool EDGE, bool WT>
 __device__ __forceinline__ void rp_rec_get(const double* __restrict__ rec, int64_t n,
-                                           int64_t ktot, int64_t ea, int64_t ec, double2& j01,
-                                           double& j2) {
+                                           int64_t ktot, int64_t ea, int64_t ec, double* j) {
   const double* row = rec + n * rec_ld(ktot);
   if constexpr (WT) {
     const __amdgpu_buffer_rsrc_t r = wt_rsrc(row + ec);
     const uint32_t o = uint32_t(ea - ec) * 8u;
     if constexpr (!EDGE) {
-      j01 = wt_ld16(r, o);
-      j2 = wt_ld8(r, o + 16u);
+#pragma unroll
+      for (int q = 0; q < E; q += 2) {
+        const double2 v = wt_ld16(r, o + 8u * q);
+        j[q] = v.x;
+        j[q + 1] = v.y;
+      }
+      j[E] = wt_ld8(r, o + 8u * E);
     } else {
-      j01.x = (ea >= 0 && ea < ktot) ? wt_ld8(r, o) : 0.0;
-      j01.y = (ea + 1 >= 0 && ea + 1 < ktot) ? wt_ld8(r, o + 8u) : 0.0;
-      j2 = (ea + 2 >= 0 && ea + 2 < ktot) ? wt_ld8(r, o + 16u) : 0.0;
+#pragma unroll
+      for (int m = 0; m <= E; ++m) j[m] = (ea + m >= 0 && ea + m < ktot) ? wt_ld8(r, o + 8u * m) : 0.0;
     }
   } else {
     if constexpr (!EDGE) {
-      j01 = *reinterpret_cast<const double2*>(row + ea);
-      j2 = row[ea + 2];
+#pragma unroll
+      for (int q = 0; q < E; q += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(row + ea + q);
+        j[q] = v.x;
+        j[q + 1] = v.y;
+      }
+      j[E] = row[ea + E];
     } else {
-      j01.x = (ea >= 0 && ea < ktot) ? row[ea] : 0.0;
-      j01.y = (ea + 1 >= 0 && ea + 1 < ktot) ? row[ea + 1] : 0.0;
-      j2 = (ea + 2 >= 0 && ea + 2 < ktot) ? row[ea + 2] : 0.0;
+#pragma unroll
+      for (int m = 0; m <= E; ++m) j[m] = (ea + m >= 0 && ea + m < ktot) ? row[ea + m] : 0.0;
     }
   }
 }
@@ -352,7 +368,8 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
   constexpr int T = G::T, LB = G::LB;
   constexpr int H = RpHalo<MS>::F;  // the level cone + the final state's neighbours, even
   constexpr int TE = T - 2 * H;
-  static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && E == 2, "pair tiles: aligned pairs");
+  static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && (E == 2 || E == 4),
+                "pair tiles: aligned pairs");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO;
   constexpr int CB = G::kLds;  // lds[CB + i] = bnd[i] (edge tiles)
   constexpr int CR = CB + MS * 5;  // the record's inflow values
@@ -381,7 +398,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
     // u^{n0}'s left-face jumps (record n0-1) from the staged nodal values, as step_tile
     jv[m] = us[0] - ((EDGE && El[m].first) ? lds[CR] : us[-1]);
   }
-  if (n0 >= 1) rp_rec_put<EDGE, WT>(rec, n0 - 1, c.ktot, El, jv[0], jv[1], ec);
+  if (n0 >= 1) rp_rec_put<E, EDGE, WT>(rec, n0 - 1, c.ktot, El, jv, ec);
   __syncthreads();  // the image is read: the face arrays alias it
 
   const double b4 = c.beta[4], b5 = c.beta[5], b3 = c.beta[3], b2 = c.beta[2];
@@ -496,7 +513,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
           }
         }
       }
-      if (l == 0 && st >= 1) rp_rec_put<EDGE, WT>(rec, n0 + st - 1, c.ktot, El, jv[0], jv[1], ec);
+      if (l == 0 && st >= 1) rp_rec_put<E, EDGE, WT>(rec, n0 + st - 1, c.ktot, El, jv, ec);
     }
   }
   if (jend) {
@@ -519,7 +536,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
       if constexpr (EDGE) uL = El[m].first ? lds[CR + MS] : uL;
       jv[m] = u0[m] - uL;
     }
-    rp_rec_put<EDGE, WT>(rec, n0 + MS - 1, c.ktot, El, jv[0], jv[1], ec);
+    rp_rec_put<E, EDGE, WT>(rec, n0 + MS - 1, c.ktot, El, jv, ec);
   }
   __syncthreads();  // the last face reads are done: the image is rewritten
   rp_store<NP, NW, E, H, EDGE, WT>(last, tile * TE * NP, nd, lds, ue, uo, false);
@@ -571,7 +588,8 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
   constexpr int T = G::T, LB = G::LB;
   constexpr int H = RpHalo<MS>::A;
   constexpr int TE = T - 2 * H;
-  static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && E == 2, "pair tiles: aligned pairs");
+  static_assert(TE % 2 == 0 && TE > 0 && H % 2 == 0 && (E == 2 || E == 4),
+                "pair tiles: aligned pairs");
   constexpr int NE = EOArgs<NP>::NE, NO = EOArgs<NP>::NO, N = NP - 1;
   constexpr int FB = LB + 2;
   const int lane = threadIdx.x;
@@ -584,9 +602,8 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
   const int off = rp_load<NP, NW, E, EDGE, WT>(win, e0, nd, lds);
   // the left-face jumps of u^{n0+st+1} (record n0+st) of the lane's two elements and of its
   // right neighbour: one 16-byte and one 8-byte load per lane and step, prefetched a step ahead
-  double2 jn;
-  double jn2;
-  rp_rec_get<EDGE, WT>(rec, n0 + MS - 1, c.ktot, ea, ec, jn, jn2);
+  double jn[E + 1];
+  rp_rec_get<E, EDGE, WT>(rec, n0 + MS - 1, c.ktot, ea, ec, jn);
   __syncthreads();
   double we[E][NE], wo[E][NO];
   Elem El[E];
@@ -615,7 +632,9 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
     // du0 = j_e; du1 = -j_{e+1} (0 at a trajectory's last element): du0 - du1 and du0 + du1
     // are the snapshot path's doubles bit for bit (dg_common.h rec_ld).  The next step's
     // record is loaded after this step's indicator has read the current one.
-    const double jc[E + 1] = {jn.x, jn.y, jn2};
+    double jc[E + 1];
+#pragma unroll
+    for (int m = 0; m <= E; ++m) jc[m] = jn[m];
     if (has_eta) {
 #pragma unroll
       for (int m = 0; m < E; ++m) {
@@ -632,7 +651,7 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
         eacc[m] += cc;
       }
     }
-    if (st > 0) rp_rec_get<EDGE, WT>(rec, n0 + st - 1, c.ktot, ea, ec, jn, jn2);
+    if (st > 0) rp_rec_get<E, EDGE, WT>(rec, n0 + st - 1, c.ktot, ea, ec, jn);
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
       // buffers alternate over the launch's global level index (no barrier between a step's

@@ -165,10 +165,9 @@ template <int NP, bool UNI> struct SweepOcc {
   static constexpr int waves_per_simd = (UNI && NP <= 5) ? 6 : 1;  // 1: no constraint
 };
 
-template <int NP, bool UNI, int NW, int MSF, int MSA>
+template <int NP, bool UNI, int NW, int MSF, int MSA, int E>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
-    SweepOcc<NP, UNI>::waves_per_simd))) void k_sweep_rp(SweepArgs<NP, MSF> a) {
-  constexpr int E = 2;
+    E == 2 ? SweepOcc<NP, UNI>::waves_per_simd : 1))) void k_sweep_rp(SweepArgs<NP, MSF> a) {
   using G = RpGeo<NP, NW, E>;
   constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
   constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;
@@ -243,7 +242,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
       const int64_t e0 = int64_t(j) * TEF - HF;
       using SA = SweepArgs<NP, MSF>;
       const double* kb = reinterpret_cast<const double*>(
-                             kernarg_tail<decltype(&k_sweep_rp<NP, UNI, NW, MSF, MSA>), SA>() +
+                             kernarg_tail<decltype(&k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), SA>() +
                              offsetof(SA, bnd)) + blk * (MSF * 6 + 1);
       const int64_t n0 = int64_t(blk) * MSF;
       const bool jend = blk == a.nbF - 1;
@@ -344,7 +343,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
 
 static_assert(kSweepMaxBlocks + 1 == sizeof(SweepBufs::U) / sizeof(double*), "SweepBufs");
 
-template <int NP, bool UNI, int NW, int MSF, int MSA>
+template <int NP, bool UNI, int NW, int MSF, int MSA, int E>
 int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int nsteps,
                  int mode, hipStream_t st) {
   SweepArgs<NP, MSF> a;
@@ -372,7 +371,7 @@ int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int 
   a.am_pi = b.am_pi;
   a.nbF = nbF;
   a.nbA = nbA;
-  using G = RpGeo<NP, NW, 2>;
+  using G = RpGeo<NP, NW, E>;
   a.nTF = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSF>::F));
   a.nTA = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSA>::A));
   a.nsteps = nsteps;
@@ -380,34 +379,41 @@ int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int 
   a.err_host = b.err_host;
   a.spin_limit = b.spin_limit > 0 ? b.spin_limit : kSweepSpinLimit;
   const int64_t items = int64_t(nbF) * a.nTF + int64_t(nbA) * a.nTA;
-  hipLaunchKernelGGL((k_sweep_rp<NP, UNI, NW, MSF, MSA>), dim3(unsigned(items)), dim3(64 * NW), 0,
+  hipLaunchKernelGGL((k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), dim3(unsigned(items)), dim3(64 * NW), 0,
                      st, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
 
-template <int NP, bool UNI, int NW>
+template <int NP, bool UNI, int NW, int E>
 int sweep_shape_launch(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0,
                        double dt, int nsteps, int mode, hipStream_t st) {
+  if constexpr (NW > 8) {  // the wide tiles: 20- or 10-step forward, 10-step adjoint blocks
+    if (msa == 10 && msf == 20) return sweep_launch<NP, UNI, NW, 20, 10, E>(p, b, t0, dt, nsteps, mode, st);
+    if (msa == 10 && msf == 10) return sweep_launch<NP, UNI, NW, 10, 10, E>(p, b, t0, dt, nsteps, mode, st);
+    return fail(DG_ERR_ARG, "dataflow sweep: 12 or 16 waves take 10- or 20-step forward and "
+                            "10-step adjoint blocks");
+  }
   if (msa == 10) {
-    if constexpr (NW == 8)
-      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 10>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 10>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 10>(p, b, t0, dt, nsteps, mode, st);
+    if constexpr (NW * E >= 16)  // 20-step forward blocks need 1024-element tiles
+      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 10, E>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 10, E>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 10, E>(p, b, t0, dt, nsteps, mode, st);
   } else if (msa == 5) {
-    if constexpr (NW == 8)
-      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 5>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 5>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 5>(p, b, t0, dt, nsteps, mode, st);
+    if constexpr (NW * E >= 16)  // 20-step forward blocks need 1024-element tiles
+      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 5, E>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 5, E>(p, b, t0, dt, nsteps, mode, st);
+    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 5, E>(p, b, t0, dt, nsteps, mode, st);
   }
   return fail(DG_ERR_ARG, "dataflow sweep: unsupported steps per block for this tile width");
 }
 
-template <int NP, int NW>
+template <int NP, int NW, int E = 2>
 int sweep_uni(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0, double dt,
               int nsteps, int mode, hipStream_t st) {
-  return p->uniform ? sweep_shape_launch<NP, true, NW>(p, msf, msa, b, t0, dt, nsteps, mode, st)
-                    : sweep_shape_launch<NP, false, NW>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+  return p->uniform
+             ? sweep_shape_launch<NP, true, NW, E>(p, msf, msa, b, t0, dt, nsteps, mode, st)
+             : sweep_shape_launch<NP, false, NW, E>(p, msf, msa, b, t0, dt, nsteps, mode, st);
 }
 
 // Tiles of 128 * waves elements on workgroups of `waves` waves: 8 (1024 elements, the
@@ -418,9 +424,19 @@ int sweep_uni(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0, 
 template <int NP>
 int sweep_np(dg_plan* p, int waves, int msf, int msa, const dgk::SweepBufs& b, double t0,
              double dt, int nsteps, int mode, hipStream_t st) {
+  if constexpr (NP <= 3) {  // four elements per lane (DG_TUNE_SWEEP_LANE_ELEMENTS)
+    if (p->sweep_lane_elems == 4) {
+      if (waves == 8) return sweep_uni<NP, 8, 4>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+      if (waves == 4) return sweep_uni<NP, 4, 4>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+      return fail(DG_ERR_ARG, "dataflow sweep: four elements per lane on 4 or 8 waves");
+    }
+  }
   if (waves == 8) return sweep_uni<NP, 8>(p, msf, msa, b, t0, dt, nsteps, mode, st);
   if (waves == 4) return sweep_uni<NP, 4>(p, msf, msa, b, t0, dt, nsteps, mode, st);
-  return fail(DG_ERR_ARG, "dataflow sweep: workgroups of 4 or 8 waves");
+  if (waves == 12) return sweep_uni<NP, 12>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+  if constexpr (NP <= 5)  // 2048 * Np doubles of LDS; larger Np would not fit 4 waves per SIMD
+    if (waves == 16) return sweep_uni<NP, 16>(p, msf, msa, b, t0, dt, nsteps, mode, st);
+  return fail(DG_ERR_ARG, "dataflow sweep: workgroups of 4, 8, 12 or 16 (Np <= 5) waves");
 }
 
 }  // namespace
@@ -428,14 +444,14 @@ int sweep_np(dg_plan* p, int waves, int msf, int msa, const dgk::SweepBufs& b, d
 namespace dgk {
 
 int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps) {
-  const int T = 128 * waves;
+  const int T = 64 * p->sweep_lane_elems * waves;
   const int64_t nTF = grid_for(p->ktot, T - 2 * ((msf * 5 + 2) & ~1));
   const int64_t nTA = grid_for(p->ktot, T - 2 * ((msa * 5 + 1) & ~1));
   return int64_t(nsteps / msf) * nTF + int64_t(nsteps / msa) * nTA;
 }
 
 int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa) {
-  return grid_for(p->ktot, 128 * waves - 2 * ((msa * 5 + 1) & ~1));
+  return grid_for(p->ktot, 64 * p->sweep_lane_elems * waves - 2 * ((msa * 5 + 1) & ~1));
 }
 
 int sweep_launch_rec(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,

@@ -136,7 +136,8 @@ class DGAdvection1D:
 
   def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None,
            rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
-           rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None, rec_sweep=None):
+           rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None, rec_sweep=None,
+           sweep_waves=None, sweep_lane_elements=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -151,13 +152,18 @@ class DGAdvection1D:
     ``rec_fwd_tile_width`` likewise gives the forward its own tile width (0: the adjoint's;
     setting ``rec_tile_width`` applies to both).  ``rec_sweep`` (1, default / 0): ``sweep_rec``
     runs both directions as one dataflow launch where the shape allows, or as the two launch
-    chains (bit-identical)."""
+    chains (bit-identical).  ``sweep_waves`` (0 / 4 / 8 / 12 / 16): the dataflow launch's
+    workgroup waves, tiles of 128 * waves elements in both directions (0: as the record tile
+    width; bit-identical at any value); ``sweep_lane_elements`` (2, or 4 at N <= 2): consecutive
+    elements per lane of its tiles."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
                      (_lib.DG_TUNE_REC_SWEEP, rec_sweep),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
                      (_lib.DG_TUNE_REC_LANE_ELEMENTS, rec_lane_elements),
                      (_lib.DG_TUNE_REC_FWD_STEPS_PER_LAUNCH, rec_fwd_steps_per_launch),
-                     (_lib.DG_TUNE_REC_FWD_TILE_WIDTH, rec_fwd_tile_width)):
+                     (_lib.DG_TUNE_REC_FWD_TILE_WIDTH, rec_fwd_tile_width),
+                     (_lib.DG_TUNE_SWEEP_WAVES, sweep_waves),
+                     (_lib.DG_TUNE_SWEEP_LANE_ELEMENTS, sweep_lane_elements)):
       if val is not None:
         _lib.check(self._lib.dg_plan_tune(self._plan, key, int(val)), "dg_plan_tune")
     if xcd_order is not None:
@@ -387,6 +393,13 @@ class DGAdvection1D:
     _lib.check(self._lib.dg_sweep_status(self._plan, ctypes.byref(st), _stream(self.device)),
                "dg_sweep_status")
     return int(st.value)
+
+  def set_tvb(self, M):
+    """The TVB constant of ``slope_limit`` / ``slope_limit_1`` (utils/minmodB.m: the element's
+    own slope is kept unless |ux| > M h^2); 0 restores the plain minmod (dg_plan_set_tvb)."""
+    _lib.check(self._lib.dg_plan_set_tvb(self._plan, float(M)), "dg_plan_set_tvb")
+    self.tvb_M = float(M)
+    return self
 
   def slope_limit(self, u, out=None, ids=None):
     """SlopeLimitN(u) (utils/SlopeLimitN.m:1-33); ids (int32, batch*K) marks limited cells."""

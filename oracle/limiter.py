@@ -49,18 +49,21 @@ def cell_average(u, S):
   return S["V"][0, 0] * uh0, uh0
 
 
-def slope_limit_lin(ul, xl, vm1, v0, vp1, S):
-  """utils/SlopeLimitLin.m:10-18."""
+def slope_limit_lin(ul, xl, vm1, v0, vp1, S, M=None):
+  """utils/SlopeLimitLin.m:10-18; with M (> 0) its minmod is minmodB(., M, h), the TVB variant
+  (utils/minmodB.m:6-11, which the reference defines but none of its limiters calls)."""
   Np = S["Np"]
   h = xl[Np - 1, :] - xl[0, :]  # :10
   x0 = xl[0, :] + h / 2  # :11
   ux0 = (2.0 / h) * _row_dot(S["Dr"][0, :], ul)  # :16 (row 1 of (2./hN).*(Dr*ul))
-  m = minmod(np.vstack((ux0, (vp1 - v0) / h, (v0 - vm1) / h)))  # :18
+  args = np.vstack((ux0, (vp1 - v0) / h, (v0 - vm1) / h))
+  m = minmod_b(args, M, h) if M else minmod(args)  # :18
   return v0[None, :] + (xl - x0[None, :]) * m[None, :]
 
 
-def slope_limit_n(u, S, return_ids=False):
-  """utils/SlopeLimitN.m:1-33 for one trajectory (u is (Np, K))."""
+def slope_limit_n(u, S, return_ids=False, M=None):
+  """utils/SlopeLimitN.m:1-33 for one trajectory (u is (Np, K)); M: the TVB constant of the
+  SlopeLimitLin it calls (slope_limit_lin)."""
   K = u.shape[1]
   v, uh0 = cell_average(u, S)  # :9
   ulimit = u.copy()
@@ -77,14 +80,14 @@ def slope_limit_n(u, S, return_ids=False):
     uh1 = _row_dot(S["invV"][1, :], uid)
     V = S["V"]
     ul = V[:, 0:1] * uh0[None, ids] + V[:, 1:2] * uh1[None, :]  # :28 (uhl(3:Np,:)=0)
-    ulimit[:, ids] = slope_limit_lin(ul, S["x"][:, ids], vkm1[ids], vk[ids], vkp1[ids], S)
+    ulimit[:, ids] = slope_limit_lin(ul, S["x"][:, ids], vkm1[ids], vk[ids], vkp1[ids], S, M)
   if return_ids:
     return ulimit, ids
   return ulimit
 
 
-def slope_limit_1(u, S):
-  """utils/SlopeLimit1.m:6-22 — Pi^1 limiter applied to every cell."""
+def slope_limit_1(u, S, M=None):
+  """utils/SlopeLimit1.m:6-22 — Pi^1 limiter applied to every cell (M: as slope_limit_n)."""
   K = u.shape[1]
   v, uh0 = cell_average(u, S)
   uh1 = _row_dot(S["invV"][1, :], u)
@@ -92,4 +95,4 @@ def slope_limit_1(u, S):
   ul = V[:, 0:1] * uh0[None, :] + V[:, 1:2] * uh1[None, :]
   vkm1 = np.concatenate(([v[0]], v[:K - 1]))
   vkp1 = np.concatenate((v[1:], [v[K - 1]]))
-  return slope_limit_lin(ul, S["x"], vkm1, v, vkp1, S)
+  return slope_limit_lin(ul, S["x"], vkm1, v, vkp1, S, M)

@@ -273,6 +273,36 @@ def test_slope_limiter_matches_SlopeLimit1(pkg, gpu, N):
   np.testing.assert_allclose(setup1d.from_elem_major(got, N + 1), ref, rtol=0, atol=1e-13)
 
 
+@pytest.mark.parametrize("N,M", [(1, 3e6), (2, 1e6), (4, 3e6), (8, 1e7)])
+def test_slope_limiter_tvb_matches_minmodB(pkg, gpu, N, M):
+  """dg_plan_set_tvb(M): SlopeLimitLin's minmod becomes utils/minmodB.m (the element's own
+  slope kept where |ux| <= M h^2) in dg_slope_limit_n and dg_slope_limit_1, against the oracle
+  with the same M; M chosen so that both branches occur (h = 1/517: M h^2 ~ 4..40 against
+  slopes ~ 2 pi .. 50); M = 0 restores the plain limiter bit for bit."""
+  import torch
+  rng = np.random.default_rng(200 + N)
+  K = 517
+  S, mesh = mesh_pair(pkg, N, K)
+  u = _limiter_input(rng, S)
+  op = make_op(pkg, mesh)
+  ud = dev(setup1d.to_elem_major(u), gpu)
+  plain_n, plain_1 = host(op.slope_limit(ud)), host(op.slope_limit_1(ud))
+  op.set_tvb(M)
+  ref_n, ids_ref = olim.slope_limit_n(u, S, return_ids=True, M=M)
+  ref_1 = olim.slope_limit_1(u, S, M=M)
+  ids = torch.zeros(K, dtype=torch.int32, device=gpu)
+  got_n = host(op.slope_limit(ud, ids=ids))
+  got_1 = host(op.slope_limit_1(ud))
+  np.testing.assert_array_equal(np.nonzero(host(ids))[0], ids_ref)
+  np.testing.assert_allclose(setup1d.from_elem_major(got_n, N + 1), ref_n, rtol=0, atol=1e-13)
+  np.testing.assert_allclose(setup1d.from_elem_major(got_1, N + 1), ref_1, rtol=0, atol=1e-13)
+  kept = np.any(np.abs(setup1d.from_elem_major(got_1 - plain_1, N + 1)) > 1e-12, axis=0)
+  assert 0 < kept.sum() < K, kept.sum()  # TVB kept some slopes, minmod limited others
+  op.set_tvb(0.0)
+  np.testing.assert_array_equal(host(op.slope_limit(ud)), plain_n)
+  np.testing.assert_array_equal(host(op.slope_limit_1(ud)), plain_1)
+
+
 # ---------------------------------------------------------------------------
 def test_argmax_numpy_semantics(pkg, gpu):
   S, mesh = mesh_pair(pkg, 2, 4000)

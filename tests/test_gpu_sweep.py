@@ -402,3 +402,64 @@ def test_alternating_shapes_keep_refine_aligned(pkg, gpu):
       torch.cuda.synchronize()
       assert host(got)[:2].tolist() == host(ref)[:2].tolist(), (rep, asteps)
   assert op.sweep_status() == 0
+
+
+@pytest.mark.parametrize("N,K,batch,waves,fsteps,nsteps", [
+    (4, 9000, 1, 12, 20, 20),   # 1536-element tiles
+    (4, 7000, 2, 16, 20, 20),   # 2048-element tiles, trajectory edges inside tiles
+    (1, 9000, 1, 16, 10, 20),
+    (8, 6000, 1, 12, 20, 20),   # Np = 9: the launch chains run 1024 forward / 512 adjoint tiles
+    (6, 5000, 1, 12, 10, 40),
+])
+def test_wide_dataflow_tiles_equal_launch_chains(pkg, gpu, N, K, batch, waves, fsteps, nsteps):
+  """DG_TUNE_SWEEP_WAVES = 12 / 16: the dataflow launch on tiles of 1536 / 2048 elements in both
+  directions (also where the launch chains' forward and adjoint widths differ, Np = 9) gives
+  the launch chains' bits: every element's arithmetic is the same on any tile."""
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh, batch=batch)
+  op.tune(rec_steps_per_launch=10, rec_fwd_steps_per_launch=fsteps)
+  if N == 8:
+    op.tune(rec_tile_width=1, rec_fwd_tile_width=2)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 60 + N, batch)
+  ref = run_sweep(op, u0, dt, nsteps, False)
+  op.tune(sweep_waves=waves, rec_sweep=1)
+  on, f, a, items, w, T = op.query_sweep(nsteps, tile=True)
+  assert on and (f, a, w, T) == (fsteps, 10, waves, 128 * waves)
+  got = run_sweep(op, u0, dt, nsteps, True)
+  assert_same(got, ref, f"{waves} waves, N={N}")
+
+
+@pytest.mark.parametrize("N,K,batch,waves,fsteps,nsteps,inflow", [
+    (1, 9000, 1, 8, 20, 20, "a"),    # 2048-element tiles
+    (1, 3001, 3, 8, 10, 20, "a2"),   # trajectory edges inside tiles, odd element count
+    (2, 7000, 1, 4, 20, 40, "a"),    # 1024-element tiles on 4 waves
+    (2, 2500, 2, 8, 10, 30, "zero"),
+])
+def test_four_elements_per_lane_equal_launch_chains(pkg, gpu, N, K, batch, waves, fsteps, nsteps,
+                                                    inflow):
+  """DG_TUNE_SWEEP_LANE_ELEMENTS = 4 (Np <= 3): the dataflow launch with four consecutive
+  elements per lane (two 16-byte record accesses per lane and step) gives the launch chains'
+  bits."""
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
+  op.tune(rec_steps_per_launch=10, rec_fwd_steps_per_launch=fsteps)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 70 + N, batch)
+  ref = run_sweep(op, u0, dt, nsteps, False)
+  op.tune(sweep_waves=waves, sweep_lane_elements=4, rec_sweep=1)
+  on, f, a, items, w, T = op.query_sweep(nsteps, tile=True)
+  assert on and (f, a, w, T) == (fsteps, 10, waves, 256 * waves)
+  got = run_sweep(op, u0, dt, nsteps, True)
+  assert_same(got, ref, f"4 elements per lane, N={N}, {waves} waves")
+  # and the fused refine decision on these tiles
+  import torch
+  rec, w_ = op.new_jumps(nsteps), op.new_field()
+  eta = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+  res = torch.zeros(3, dtype=torch.int64, device=gpu)
+  if batch == 1:
+    op.sweep_refine(u0, rec, w_, 0.0, dt, nsteps, eta, res[0:1], res[1:2].view(torch.float64),
+                    res[2:3])
+    torch.cuda.synchronize()
+    e = np.abs(host(eta))
+    assert int(host(res)[0]) == int(np.argmax(e)) and op.sweep_status() == 0

@@ -161,3 +161,28 @@ def test_sum_rows_and_argmax_semantics():
   assert oadj.argmax([1.0, 3.0, 3.0]) == 1
   assert oadj.argmax([1.0, np.nan, 5.0, np.nan]) == 1
   assert oadj.argmax([1.0, -5.0, 4.0], use_abs=True) == 1
+
+
+def test_tvb_slope_limiter_reduces_to_minmod_and_keeps_small_slopes():
+  """oracle slope_limit_n / slope_limit_1 with the TVB constant (utils/minmodB.m:6-11): M = 0
+  is the plain minmod; a huge M keeps every cell's own linear slope (SlopeLimitLin then only
+  projects to the linear part); intermediate M switches per cell on |ux| > M h^2."""
+  from oracle import limiter as olim
+  from oracle import setup1d
+  rng = np.random.default_rng(5)
+  S = setup1d.uniform_setup(3, 200, metric="element")
+  x = S["x"]
+  u = np.sin(2 * np.pi * x) + (x > 0.5) + 0.02 * rng.standard_normal(x.shape)
+  np.testing.assert_array_equal(olim.slope_limit_1(u, S, M=0.0), olim.slope_limit_1(u, S))
+  big = olim.slope_limit_1(u, S, M=1e30)
+  # the Pi^1 projection of u: cell average + linear mode, i.e. SlopeLimitLin with m = ux
+  v, uh0 = olim.cell_average(u, S)
+  uh1 = olim._row_dot(S["invV"][1, :], u)
+  V = S["V"]
+  ul = V[:, 0:1] * uh0[None, :] + V[:, 1:2] * uh1[None, :]
+  np.testing.assert_allclose(big, ul, atol=1e-12)
+  h = x[-1, :] - x[0, :]
+  mid = olim.slope_limit_1(u, S, M=1e5)
+  plain = olim.slope_limit_1(u, S)
+  differs = np.any(np.abs(mid - plain) > 1e-12, axis=0)
+  assert 0 < differs.sum() < u.shape[1]
