@@ -1162,17 +1162,36 @@ inline int chunk(const dg_plan* p, int left) {
 // With the plan's sweep_waves set (DG_TUNE_SWEEP_WAVES) the dataflow launch runs both
 // directions on tiles of 128 * sweep_waves elements, whatever the launch chains' widths: 12
 // and 16 waves take the 10- or 20-step forward and 10-step adjoint blocks (16 at Np <= 5).
+// Unset (0), the shape follows the record sweeps' tile width, with the measured exceptions
+// below (12-wave tiles at Np <= 5, 8-wave tiles at Np = 9 on uniform meshes).
 bool sweep_shape(const dg_plan* p, int nsteps, int* waves, int* msf, int* msa) {
   const int f = rec_msteps_fwd(p), a = rec_msteps(p), w = p->rec_tile_width;
   const int sw = p->sweep_waves;
-  const int nw = sw ? sw : 4 * w;
+  int nw = sw;
+  bool tiles;
+  if (sw) {
+    tiles = (sw == 4 || sw == 8) || ((sw == 12 || (sw == 16 && p->NP <= 5)) && f >= 10 && a == 10);
+  } else if (p->NP == 9 && p->uniform) {
+    // the launch chains run 1024-element forward and 512-element adjoint tiles here; the one
+    // launch takes 8-wave (1024-element) tiles in both directions: 7.06-7.23e11 DOF-updates/s
+    // at K = 2^20 against 6.65e11 for the chains (profiles/r04/opreload/)
+    nw = 8;
+    tiles = true;
+  } else {
+    // as the record sweeps' tile width; on the 6-wave-per-SIMD uniform bodies (Np <= 5) 12-wave
+    // tiles where their shape allows (1536 elements, 2 workgroups per CU; forward halo 1.15
+    // instead of 1.25, a third fewer items): +3-4 % at N = 4, +1-3 % at N = 2, equal at N = 1
+    // (profiles/r04/take/, perN/, shape_ab/)
+    nw = 4 * w;
+    tiles = rec_fwd_width(p) == w && (w == 1 || w == 2);
+    if (tiles && w == 2 && p->uniform && p->NP <= 5 && p->sweep_lane_elems == 2 && f >= 10 &&
+        a == 10)
+      nw = 12;
+  }
   *msf = f;
   *msa = a;
   *waves = nw;
-  const bool tiles = (sw ? ((sw == 4 || sw == 8) ||
-                            ((sw == 12 || (sw == 16 && p->NP <= 5)) && f >= 10 && a == 10))
-                         : (rec_fwd_width(p) == w && (w == 1 || w == 2))) &&
-                     (p->sweep_lane_elems == 2 || (p->NP <= 3 && (nw == 4 || nw == 8)));
+  tiles = tiles && (p->sweep_lane_elems == 2 || (p->NP <= 3 && (nw == 4 || nw == 8)));
   const int T = 64 * p->sweep_lane_elems * nw;  // elements per tile
   return p->rec_sweep && rec_pairs(p) && tiles &&
          (f == 5 || f == 10 || (f == 20 && T >= 1024)) && (a == 5 || a == 10) && nsteps > 0 &&
@@ -1354,6 +1373,10 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     const int k = std::atoi(v);
     if (k == 2 || (k == 4 && p->NP <= 3)) p->sweep_lane_elems = k;
   }
+  if (const char* v = std::getenv("DG_SWEEP_TAKE")) {
+    const int k = std::atoi(v);
+    if (k == 0 || k == 1) p->sweep_take = k;
+  }
   if (const char* v = std::getenv("DG_SWEEP_WAVES")) {
     const int k = std::atoi(v);
     if (k == 0 || k == 4 || k == 8 || k == 12 || (k == 16 && p->NP <= 5)) p->sweep_waves = k;
@@ -1489,6 +1512,10 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       if (!(value == 2 || (value == 4 && p->NP <= 3)))
         return fail(DG_ERR_ARG, "sweep lane elements: 2, or 4 at Np <= 3");
       p->sweep_lane_elems = int(value);
+      return DG_OK;
+    case DG_TUNE_SWEEP_TAKE:
+      if (value != 0 && value != 1) return fail(DG_ERR_ARG, "sweep take: 0 (counter) or 1 (workgroup id)");
+      p->sweep_take = int(value);
       return DG_OK;
     case DG_TUNE_SWEEP_SPIN_LIMIT:
       if (value < 0 || value > (1 << 30)) return fail(DG_ERR_ARG, "spin limit: 0 (default) .. 2^30");
@@ -1887,7 +1914,7 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   if (const int rc = sweep_scratch(p, sync_bytes, bytes - sync_bytes, st, &data)) return rc;
   const uint64_t sig = uint64_t(items) * 1000003u ^ (uint64_t(waves) << 56) ^
                       (uint64_t(msf) << 48) ^ (uint64_t(msa) << 40) ^ (uint64_t(nsteps) << 32) ^
-                      uint64_t(sweep_tiles_adj(p, waves, msa));
+                      uint64_t(sweep_tiles_adj(p, waves, msa)) ^ (uint64_t(p->sweep_take) << 62);
   if (p->sweep_items != items || p->sweep_sig != sig) {
     // the take counter numbers launches by items per launch and the fused refine's arrival
     // counter by the last block's tiles: a new shape starts both afresh
@@ -1923,6 +1950,7 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   b.am_pi = idx ? reinterpret_cast<int64_t*>(am + am_parts) : nullptr;
   b.err_host = p->d_sweep_err;
   b.spin_limit = p->sweep_spin_limit;
+  b.take = p->sweep_take;
   const int mode = eta ? (kEtaOn | ((aflags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
                           ((aflags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
                        : 0;

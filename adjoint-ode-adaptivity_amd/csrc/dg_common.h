@@ -84,6 +84,15 @@ __device__ __forceinline__ const char* kernarg_tail() {
   return (const char*)__builtin_amdgcn_kernarg_segment_ptr() + L::kTailOffset;
 }
 
+// The same tail as a constant-address-space (kernarg) pointer: loads through it are scalar
+// loads, also after the pointer is laundered (dg_rec_tiles.h OpSrc).
+#define DG_KAS __attribute__((address_space(4)))
+template <class F, class A>
+__device__ __forceinline__ const DG_KAS char* kernarg_tail_k() {
+  (void)kernarg_tail<F, A>();  // the layout checks
+  return (const DG_KAS char*)__builtin_amdgcn_kernarg_segment_ptr() + KernargLayout<F>::kTailOffset;
+}
+
 // Sets the calling thread's dg_last_error() text and returns `code` (dg_advec.hip).
 int fail(int code, const std::string& msg);
 
@@ -478,6 +487,9 @@ struct dg_plan {
   // consecutive elements per lane of the dataflow sweep's tiles: 2 (pair tiles), or 4 at
   // Np <= 3 on 4- or 8-wave workgroups (tiles of 64 * 4 * waves elements)
   int sweep_lane_elems = 2;
+  // how a dataflow workgroup gets its item: 0 the take counter, 1 its workgroup id (the
+  // epoch from the item's own flag)
+  int sweep_take = 0;
   uint64_t* sweep_trace = nullptr;  // dg_plan_sweep_trace: per-item timestamps (profiling)
   int cu_count = 0;  // compute units of the plan's device (the dataflow grid)
   int xcd_order = 1;  // XCD-aware tile order
@@ -628,6 +640,7 @@ struct SweepBufs {
   int64_t* am_pi;
   uint32_t* err_host;  // nullable: the plan's host-visible watchdog flag (d_sweep_err)
   int32_t spin_limit;  // 0: the default
+  int32_t take;        // dg_plan::sweep_take
 };
 int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps);
 int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa);

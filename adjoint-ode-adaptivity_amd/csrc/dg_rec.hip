@@ -40,14 +40,17 @@ __global__ __launch_bounds__(64 * NW) void k_step_rp(const double* __restrict__ 
   const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.c.xcd);
   constexpr int H = RpHalo<MS>::F;
   const int64_t e0 = tile * (G::T - 2 * H) - H;
+  using SArgs = RpStepArgs<NP, MS>;
+  const OpSrc<NP> os = op_src<NP>(
+      args.c, kernarg_tail_k<decltype(&k_step_rp<NP, UNI, NW, E, MS>), SArgs>() + offsetof(SArgs, c));
   if (edge_tile(e0, G::T, args.c.ktot, args.c.K)) {
-    using SArgs = RpStepArgs<NP, MS>;  // lane-indexed kernarg read, see step_tile
+    // lane-indexed kernarg read, see step_tile
     const double* kb = reinterpret_cast<const double*>(
         kernarg_tail<decltype(&k_step_rp<NP, UNI, NW, E, MS>), SArgs>() + offsetof(SArgs, bnd));
-    rp_step_tile<NP, UNI, NW, E, MS, true, false>(lds, tile, uin, rec, last, scale, args.c, kb,
-                                                  args.n0, args.jend);
+    rp_step_tile<NP, UNI, NW, E, MS, true, false>(lds, tile, uin, rec, last, scale, args.c, os,
+                                                  kb, args.n0, args.jend);
   } else {
-    rp_step_tile<NP, UNI, NW, E, MS, false, false>(lds, tile, uin, rec, last, scale, args.c,
+    rp_step_tile<NP, UNI, NW, E, MS, false, false>(lds, tile, uin, rec, last, scale, args.c, os,
                                                    nullptr, args.n0, args.jend);
   }
 }
@@ -65,12 +68,15 @@ __global__ __launch_bounds__(64 * NW) void k_adj_rp(const double* __restrict__ w
   constexpr int H = RpHalo<MS>::A;
   const int64_t e0 = tile * (G::T - 2 * H) - H;
   EtaSink es{eta, nullptr, nullptr, 0, 0, args.has_eta, false, 0.0, 0};
+  using AArgs = RpAdjArgs<NP, MS>;
+  const OpSrc<NP> os = op_src<NP>(
+      args.c, kernarg_tail_k<decltype(&k_adj_rp<NP, UNI, NW, E, MS>), AArgs>() + offsetof(AArgs, c));
   if (edge_tile(e0, G::T, args.c.ktot, args.c.K))
-    rp_adj_tile<NP, UNI, NW, E, MS, true, false>(lds, tile, win, wout, rec, es, scale, args.c,
+    rp_adj_tile<NP, UNI, NW, E, MS, true, false>(lds, tile, win, wout, rec, es, scale, args.c, os,
                                                  args.n0);
   else
     rp_adj_tile<NP, UNI, NW, E, MS, false, false>(lds, tile, win, wout, rec, es, scale, args.c,
-                                                  args.n0);
+                                                  os, args.n0);
 }
 
 template <int NP, int NW, int E, int MS>

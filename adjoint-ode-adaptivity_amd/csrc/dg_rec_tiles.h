@@ -352,6 +352,36 @@ template <int NP> int rp_make_op(const dg_plan* p, double dt, RpOp<NP>* c) {
   return DG_OK;
 }
 
+// Where the tile bodies read the operator blocks (Qeo, Qoe, le, lo: 2 NE NO + NP doubles).
+// Up to Np = 5 (at most 40 SGPRs) as the kernel argument they are, which the compiler keeps in
+// SGPRs for the whole kernel.  From Np = 6 on they do not fit the SGPR file beside the rest
+// (98 SGPRs at Np = 9): kept as one hoisted argument they were spilled to VGPR lanes and read
+// back with a v_readlane per use -- 2,120 v_readlane in the Np = 9 sweep kernel, a third of
+// the VALU instructions it issued.  OpSrc<NP, true> re-reads each block from the kernarg
+// segment where it is used: scalar loads through a pointer laundered by an empty asm (so not
+// hoisted), only the block in use occupying SGPRs.
+template <int NP> constexpr bool kOpReload = NP >= 6;
+template <int NP, bool R = kOpReload<NP>> struct OpSrc {
+  const EOArgs<NP>* p;
+  __device__ __forceinline__ const EOArgs<NP>& get() const { return *p; }
+};
+template <int NP> struct OpSrc<NP, true> {
+  const DG_KAS EOArgs<NP>* p;
+  __device__ __forceinline__ const DG_KAS EOArgs<NP>& get() const {
+    const DG_KAS EOArgs<NP>* q = p;
+    asm volatile("" : "+s"(q));
+    return *q;
+  }
+};
+// kc: the RpOp argument's address in the kernarg segment (kernarg_tail_k + its offset).
+template <int NP>
+__device__ __forceinline__ OpSrc<NP> op_src(const RpOp<NP>& rc, const DG_KAS char* kc) {
+  if constexpr (kOpReload<NP>)
+    return OpSrc<NP>{reinterpret_cast<const DG_KAS EOArgs<NP>*>(kc + offsetof(RpOp<NP>, op))};
+  else
+    return OpSrc<NP>{&rc.op};
+}
+
 // Forward: MS steps of the tile; records u^{n0}..u^{n0+MS-1}'s jumps (and u^{n0+MS}'s when
 // the block ends the sweep), writes u^{n0+MS} to `last`.  Per step five Horner levels, each
 // one face exchange of its input vector v (u at level 0, t after) through LDS.  `kb` (edge
@@ -362,8 +392,8 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
                                              const double* __restrict__ uin,
                                              double* __restrict__ rec, double* __restrict__ last,
                                              const double* __restrict__ scale,
-                                             const RpOp<NP>& c, const double* kb, int64_t n0,
-                                             bool jend) {
+                                             const RpOp<NP>& c, OpSrc<NP> os,
+                                             const double* kb, int64_t n0, bool jend) {
   using G = RpGeo<NP, NW, E>;
   constexpr int T = G::T, LB = G::LB;
   constexpr int H = RpHalo<MS>::F;  // the level cone + the final state's neighbours, even
@@ -425,42 +455,54 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
       // meshes (c = beta_{4-l}; level 0 has no u term here, c = 1 from level 3 on), the bare
       // products on non-uniform ones (the metric multiplies them after the lift).
       double pe[E][NE], po[E][NO];
+      {
+        const auto& op = os.get();
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+#pragma unroll
+          for (int k = 0; k < NE; ++k) {
+            const double* vo = (l == 0) ? uo[m] : to[m];
+            double a;
+            int j0 = 0;
+            if (UNI && l >= 3) {
+              a = ue[m][k];
+            } else if (UNI && l >= 1) {
+              a = (l == 1 ? b3 : b2) * ue[m][k];
+            } else {
+              a = op.Qeo[k * NO] * vo[0];
+              j0 = 1;
+            }
+#pragma unroll
+            for (int j = j0; j < NO; ++j) a = fma(op.Qeo[k * NO + j], vo[j], a);
+            pe[m][k] = a;
+          }
+        }
+      }
+      {
+        const auto& op = os.get();
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+#pragma unroll
+          for (int k = 0; k < NO; ++k) {
+            const double* ve = (l == 0) ? ue[m] : te[m];
+            double a;
+            int j0 = 0;
+            if (UNI && l >= 3) {
+              a = uo[m][k];
+            } else if (UNI && l >= 1) {
+              a = (l == 1 ? b3 : b2) * uo[m][k];
+            } else {
+              a = op.Qoe[k * NE] * ve[0];
+              j0 = 1;
+            }
+#pragma unroll
+            for (int j = j0; j < NE; ++j) a = fma(op.Qoe[k * NE + j], ve[j], a);
+            po[m][k] = a;
+          }
+        }
+      }
 #pragma unroll
       for (int m = 0; m < E; ++m) {
-#pragma unroll
-        for (int k = 0; k < NE; ++k) {
-          const double* vo = (l == 0) ? uo[m] : to[m];
-          double a;
-          int j0 = 0;
-          if (UNI && l >= 3) {
-            a = ue[m][k];
-          } else if (UNI && l >= 1) {
-            a = (l == 1 ? b3 : b2) * ue[m][k];
-          } else {
-            a = c.op.Qeo[k * NO] * vo[0];
-            j0 = 1;
-          }
-#pragma unroll
-          for (int j = j0; j < NO; ++j) a = fma(c.op.Qeo[k * NO + j], vo[j], a);
-          pe[m][k] = a;
-        }
-#pragma unroll
-        for (int k = 0; k < NO; ++k) {
-          const double* ve = (l == 0) ? ue[m] : te[m];
-          double a;
-          int j0 = 0;
-          if (UNI && l >= 3) {
-            a = uo[m][k];
-          } else if (UNI && l >= 1) {
-            a = (l == 1 ? b3 : b2) * uo[m][k];
-          } else {
-            a = c.op.Qoe[k * NE] * ve[0];
-            j0 = 1;
-          }
-#pragma unroll
-          for (int j = j0; j < NE; ++j) a = fma(c.op.Qoe[k * NE + j], ve[j], a);
-          po[m][k] = a;
-        }
 #pragma unroll
         for (int k = 0; k < NE; ++k) pin(pe[m][k]);
 #pragma unroll
@@ -474,6 +516,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
         bnd = lds[CB + st * 5 + l];
         if (l == 0) urec = lds[CR + st];
       }
+      const auto& ol = os.get();
 #pragma unroll
       for (int m = 0; m < E; ++m) {
         double vL = (m == 0) ? fromL : vN[m - 1];
@@ -486,7 +529,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
         const double dlt = vR - vL, sig = -(vL + vR);
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
-          const double z = fma(c.op.le[k], dlt, pe[m][k]);
+          const double z = fma(ol.le[k], dlt, pe[m][k]);
           if constexpr (UNI) {
             if (l == 0) te[m][k] = fma(b5, z, b4 * ue[m][k]);
             else if (l < 4) te[m][k] = z;
@@ -500,7 +543,7 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
         }
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
-          const double z = fma(c.op.lo[k], sig, po[m][k]);
+          const double z = fma(ol.lo[k], sig, po[m][k]);
           if constexpr (UNI) {
             if (l == 0) to[m][k] = fma(b5, z, b4 * uo[m][k]);
             else if (l < 4) to[m][k] = z;
@@ -583,7 +626,7 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
                                             const double* __restrict__ rec,
                                             EtaSink& es,
                                             const double* __restrict__ scale,
-                                            const RpOp<NP>& c, int64_t n0) {
+                                            const RpOp<NP>& c, OpSrc<NP> os, int64_t n0) {
   using G = RpGeo<NP, NW, E>;
   constexpr int T = G::T, LB = G::LB;
   constexpr int H = RpHalo<MS>::A;
@@ -636,13 +679,14 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
 #pragma unroll
     for (int m = 0; m <= E; ++m) jc[m] = jn[m];
     if (has_eta) {
+      const auto& op = os.get();
 #pragma unroll
       for (int m = 0; m < E; ++m) {
         double pe = 0.0, po = 0.0;
 #pragma unroll
-        for (int k = 0; k < NE; ++k) pe = fma(c.op.le[k], we[m][k], pe);
+        for (int k = 0; k < NE; ++k) pe = fma(op.le[k], we[m][k], pe);
 #pragma unroll
-        for (int k = 0; k < NO; ++k) po = fma(c.op.lo[k], wo[m][k], po);
+        for (int k = 0; k < NO; ++k) po = fma(op.lo[k], wo[m][k], po);
         const bool lst = EDGE && El[m].last;
         const double dd = lst ? jc[m] : jc[m] + jc[m + 1];
         const double ds = lst ? jc[m] : jc[m] - jc[m + 1];
@@ -659,6 +703,7 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
       const int f0 = (((MS - 1 - st) * 5 + l) & 1) * 2 * FB, f1 = f0 + FB;
       // the level's input v (w at level 0, t after), scaled by the metric: q = sc v
       double g0[E], g1[E], qe[E][NE], qo[E][NO];
+      const auto& ol = os.get();
 #pragma unroll
       for (int m = 0; m < E; ++m) {
         double gd = 0.0, gs = 0.0;
@@ -666,13 +711,13 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
         for (int k = 0; k < NE; ++k) {
           const double v = (l == 0) ? we[m][k] : te[m][k];
           qe[m][k] = UNI ? v : sc[m] * v;
-          gd = fma(c.op.le[k], qe[m][k], gd);
+          gd = fma(ol.le[k], qe[m][k], gd);
         }
 #pragma unroll
         for (int k = 0; k < NO; ++k) {
           const double v = (l == 0) ? wo[m][k] : to[m][k];
           qo[m][k] = UNI ? v : sc[m] * v;
-          gs = fma(c.op.lo[k], qo[m][k], gs);
+          gs = fma(ol.lo[k], qo[m][k], gs);
         }
         g0[m] = gd + gs;
         g1[m] = gs - gd;
@@ -685,6 +730,7 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
       // odd outputs first (they read the even inputs, which then die), then the even ones
       // (reading the odd inputs): fewer values live at once than one loop over both
       double ae[E][NE], ao[E][NO];
+      const auto& oq = os.get();
 #pragma unroll
       for (int m = 0; m < E; ++m) {
 #pragma unroll
@@ -696,17 +742,18 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
           } else if (l >= 1) {
             t = (l == 1 ? b3 : b2) * wo[m][j];
           } else {
-            t = c.op.Qeo[j] * qe[m][0];
+            t = oq.Qeo[j] * qe[m][0];
             k0 = 1;
           }
 #pragma unroll
-          for (int k = k0; k < NE; ++k) t = fma(c.op.Qeo[k * NO + j], qe[m][k], t);
+          for (int k = k0; k < NE; ++k) t = fma(oq.Qeo[k * NO + j], qe[m][k], t);
           ao[m][j] = t;
         }
 #pragma unroll
         for (int k = 0; k < NO; ++k) pin(ao[m][k]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      const auto& or_ = os.get();
 #pragma unroll
       for (int m = 0; m < E; ++m) {
 #pragma unroll
@@ -718,11 +765,11 @@ __device__ __forceinline__ void rp_adj_tile(double* __restrict__ lds, int64_t ti
           } else if (l >= 1) {
             t = (l == 1 ? b3 : b2) * we[m][j];
           } else {
-            t = c.op.Qoe[j] * qo[m][0];
+            t = or_.Qoe[j] * qo[m][0];
             k0 = 1;
           }
 #pragma unroll
-          for (int k = k0; k < NO; ++k) t = fma(c.op.Qoe[k * NE + j], qo[m][k], t);
+          for (int k = k0; k < NO; ++k) t = fma(or_.Qoe[k * NE + j], qo[m][k], t);
           ae[m][j] = t;
         }
 #pragma unroll

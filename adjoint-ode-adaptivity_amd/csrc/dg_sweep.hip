@@ -73,6 +73,7 @@ template <int NP, int MSF> struct SweepArgs {
   int32_t nsteps;
   int32_t mode;                    // kEta* bits (0: no indicator)
   int32_t spin_limit;
+  int32_t take;                    // 0: items from the take counter; 1: item = workgroup id
 };
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
@@ -183,15 +184,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
   const int64_t nF = int64_t(nbF) * nTF;
   const int64_t nItems = nF + int64_t(nbA) * nTA;
   if (tid == 0) {
-    // The take counter only grows: every launch of this shape takes exactly nItems values
-    // (one per workgroup), so h / nItems numbers the launch (its epoch - 1) and h % nItems is
-    // the item -- no reset, no generation word, no exit counter.  (The host zeroes the
-    // control words when a launch of another shape reuses them.)
-    const uint64_t h = __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(sync + kSyncHead),
-                                              uint64_t(1), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    s_epoch = uint32_t(h / uint64_t(nItems)) + 1u;
-    s_item = uint32_t(h % uint64_t(nItems));
+    if (a.take) {
+      // item = workgroup id: each XCD starts its workgroups in id order, so the smallest
+      // unfinished item is always running or next to start on its XCD (no deadlock at any
+      // residency).  Every launch publishes every item's flag, so the item's own flag holds
+      // the previous launch's epoch: no shared counter (one contended atomic per workgroup).
+      s_item = blockIdx.x;
+      s_epoch = ld_agent(flags + blockIdx.x) + 1u;
+    } else {
+      // The take counter only grows: every launch of this shape takes exactly nItems values
+      // (one per workgroup), so h / nItems numbers the launch (its epoch - 1) and h % nItems
+      // is the item -- no reset, no generation word, no exit counter.  (The host zeroes the
+      // control words when a launch of another shape reuses them.)
+      const uint64_t h = __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(sync + kSyncHead),
+                                                uint64_t(1), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      s_epoch = uint32_t(h / uint64_t(nItems)) + 1u;
+      s_item = uint32_t(h % uint64_t(nItems));
+    }
     s_bad = 0u;
   }
   __syncthreads();
@@ -238,9 +248,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __syncthreads();
     const uint64_t t_ready = a.trace ? uint64_t(wall_clock64()) : 0;
+    using SA = SweepArgs<NP, MSF>;
+    const DG_KAS char* ka = kernarg_tail_k<decltype(&k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), SA>();
+    const OpSrc<NP> os = op_src<NP>(a.c, ka + offsetof(SA, c));
     if (fwd) {
       const int64_t e0 = int64_t(j) * TEF - HF;
-      using SA = SweepArgs<NP, MSF>;
       const double* kb = reinterpret_cast<const double*>(
                              kernarg_tail<decltype(&k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), SA>() +
                              offsetof(SA, bnd)) + blk * (MSF * 6 + 1);
@@ -248,10 +260,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
       const bool jend = blk == a.nbF - 1;
       if (edge_tile(e0, G::T, ktot, a.c.K))
         rp_step_tile<NP, UNI, NW, E, MSF, true, true>(lds, j, a.U[blk], a.rec, a.U[blk + 1],
-                                                      a.scale, a.c, kb, n0, jend);
+                                                      a.scale, a.c, os, kb, n0, jend);
       else
         rp_step_tile<NP, UNI, NW, E, MSF, false, true>(lds, j, a.U[blk], a.rec, a.U[blk + 1],
-                                                       a.scale, a.c, kb, n0, jend);
+                                                       a.scale, a.c, os, kb, n0, jend);
       if (s_bad) {  // after the body's final barrier: its stores are issued, ours follow
         const int64_t o0 = int64_t(j) * TEF * NP, nd = ktot * NP;
         poison_run<64 * NW>(a.U[blk + 1], o0, (nd - o0) < int64_t(TEF) * NP ? nd - o0
@@ -273,10 +285,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
       const int64_t n0 = int64_t(a.nsteps) - int64_t(blk + 1) * MSA;
       if (edge_tile(e0, G::T, ktot, a.c.K))
         rp_adj_tile<NP, UNI, NW, E, MSA, true, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
-                                                     a.scale, a.c, n0);
+                                                     a.scale, a.c, os, n0);
       else
         rp_adj_tile<NP, UNI, NW, E, MSA, false, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
-                                                      a.scale, a.c, n0);
+                                                      a.scale, a.c, os, n0);
       if (s_bad) {
         const int64_t o0 = int64_t(j) * TEA, nd = ktot * NP;
         const int64_t ne = (ktot - o0) < TEA ? ktot - o0 : int64_t(TEA);
@@ -378,6 +390,7 @@ int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int 
   a.mode = mode;
   a.err_host = b.err_host;
   a.spin_limit = b.spin_limit > 0 ? b.spin_limit : kSweepSpinLimit;
+  a.take = b.take;
   const int64_t items = int64_t(nbF) * a.nTF + int64_t(nbA) * a.nTA;
   hipLaunchKernelGGL((k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), dim3(unsigned(items)), dim3(64 * NW), 0,
                      st, a);

@@ -137,7 +137,7 @@ class DGAdvection1D:
   def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None,
            rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
            rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None, rec_sweep=None,
-           sweep_waves=None, sweep_lane_elements=None):
+           sweep_waves=None, sweep_lane_elements=None, sweep_take=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -155,7 +155,8 @@ class DGAdvection1D:
     chains (bit-identical).  ``sweep_waves`` (0 / 4 / 8 / 12 / 16): the dataflow launch's
     workgroup waves, tiles of 128 * waves elements in both directions (0: as the record tile
     width; bit-identical at any value); ``sweep_lane_elements`` (2, or 4 at N <= 2): consecutive
-    elements per lane of its tiles."""
+    elements per lane of its tiles; ``sweep_take`` (0 / 1): its work items from one take
+    counter or by workgroup id (bit-identical)."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
                      (_lib.DG_TUNE_REC_SWEEP, rec_sweep),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
@@ -163,7 +164,8 @@ class DGAdvection1D:
                      (_lib.DG_TUNE_REC_FWD_STEPS_PER_LAUNCH, rec_fwd_steps_per_launch),
                      (_lib.DG_TUNE_REC_FWD_TILE_WIDTH, rec_fwd_tile_width),
                      (_lib.DG_TUNE_SWEEP_WAVES, sweep_waves),
-                     (_lib.DG_TUNE_SWEEP_LANE_ELEMENTS, sweep_lane_elements)):
+                     (_lib.DG_TUNE_SWEEP_LANE_ELEMENTS, sweep_lane_elements),
+                     (_lib.DG_TUNE_SWEEP_TAKE, sweep_take)):
       if val is not None:
         _lib.check(self._lib.dg_plan_tune(self._plan, key, int(val)), "dg_plan_tune")
     if xcd_order is not None:

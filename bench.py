@@ -803,6 +803,7 @@ def main(argv=None):
     # halos rounded up to even (aligned record pairs, dg_rec.hip RpHalo), the forward's one
     # wider for the final jumps
     T_pair = sweep.op.query_sweep(nsteps, tile=True)[5] if dataflow else 512 * tw
+    sweep_waves = sweep.op.query_sweep(nsteps, tile=True)[4] if dataflow else None
     T_of = lambda m, fwd: T_pair  # noqa: E731
     h_fwd = lambda m: (5 * m + 2) & ~1  # noqa: E731
     h_adj = lambda m: (5 * m + 1) & ~1  # noqa: E731
@@ -824,6 +825,11 @@ def main(argv=None):
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
   prof_key = "p" if pmode else args.record
+  # a dataflow profile counts only for the same kernel instantiation (Np, mesh, waves, blocks)
+  kinst = (f"k_sweep_rp<{Np}, true, {sweep_waves}, {fchunks[0]}, {chunks[0]}"
+           if pairs and dataflow else None)
+  same_kernel = lambda names: kinst is None or any(  # noqa: E731
+      str(n).startswith(kinst) for n in (names or []))
   if os.path.exists(PROFILE_TRAFFIC[prof_key]):
     try:
       with open(PROFILE_TRAFFIC[prof_key]) as f:
@@ -831,7 +837,8 @@ def main(argv=None):
       if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
           and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
           and tr.get("record", "snapshots") == args.record
-          and tr.get("indicator", "jump") == args.indicator):
+          and tr.get("indicator", "jump") == args.indicator
+          and same_kernel(tr.get("adj_kernel"))):
         traffic = tr.get("adj_bytes_per_launch")
         traffic_src = tr.get("source")
     except (OSError, ValueError):
@@ -1001,7 +1008,7 @@ def main(argv=None):
       with open(PROFILE_SQ["jumps"]) as fh:
         sq = json.load(fh)
       if (N == 4 and K == (1 << 20) and sweep.batch == 1 and fchunks == [20]
-          and chunks == [10, 10] and T_pair == 1024):
+          and chunks == [10, 10] and same_kernel(sq.get("kernel"))):
         fl = sq["fp64_flops_issued_per_launch"]
         f["pmc_issued_per_launch"] = fl
         f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS

@@ -116,8 +116,11 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             workgroups of 256*value lanes, one element per lane (default 2)
  *   DG_TUNE_P_STEPS_PER_LAUNCH its steps per launch: 1, 2, 4 (default) or 8 (8 needs tile
  *                             width 2, else 4); a sweep is chunked by halving
- *   DG_TUNE_SWEEP_WAVES       workgroup waves of the dataflow sweep (dg_lserk4_sweep_rec): 0 (as
- *                             the record sweeps' tile width: 4 or 8), 4, 8, 12 or 16 (16 at
+ *   DG_TUNE_SWEEP_WAVES       workgroup waves of the dataflow sweep (dg_lserk4_sweep_rec): 0 (the
+ *                             default: as the record sweeps' tile width, 4 or 8 waves, except
+ *                             12 on uniform meshes at Np <= 5 with 1024-element record tiles,
+ *                             >= 10-step forward and 10-step adjoint blocks, and 8 on uniform
+ *                             meshes at Np = 9), 4, 8, 12 or 16 (16 at
  *                             Np <= 5); tiles of 128 * waves elements in both directions, also
  *                             where the launch chains' forward and adjoint widths differ (12
  *                             and 16 take 10- or 20-step forward and 10-step adjoint blocks).
@@ -126,19 +129,22 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             2 (default), or 4 at Np <= 3 on 4- or 8-wave workgroups (tiles
  *                             of 256 * waves elements: half the barriers per element, half the
  *                             halo share).  Bit-identical results
+ *   DG_TUNE_SWEEP_TAKE        how a dataflow work item is assigned: 0 (default) the next value
+ *                             of one take counter, 1 the workgroup id (no shared atomic; the
+ *                             launch epoch read from the item's own flag).  Bit-identical
  *   DG_TUNE_SWEEP_SPIN_LIMIT  diagnostics/tests: polls a dataflow work item makes before it
  *                             gives up waiting for a producer (0: the default, ~2^20; 1 makes
  *                             the watchdog fire on any multi-block sweep)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
  * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
- * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS. */
+ * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_TAKE. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
        DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10,
        DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12,
        DG_TUNE_SWEEP_SPIN_LIMIT = 13, DG_TUNE_SWEEP_WAVES = 14,
-       DG_TUNE_SWEEP_LANE_ELEMENTS = 15 };
+       DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch

@@ -32,7 +32,7 @@ def main():
   op = pkg.operators.DGAdvection1D(mesh)
   if a.fwd_steps:
     op.tune(rec_fwd_steps_per_launch=a.fwd_steps)
-  on, msf, msa, items = op.query_sweep(a.nsteps)
+  on, msf, msa, items, waves, T = op.query_sweep(a.nsteps, tile=True)
   assert on, "the plan does not run the dataflow sweep"
   dt = mesh.cfl_dt()
   u0 = op.new_field()
@@ -63,13 +63,13 @@ def main():
   xcc = (t[:, 3] >> 32).astype(int)
   nTF = (items - (a.nsteps // msa) * 0) and None
   nbF, nbA = a.nsteps // msf, a.nsteps // msa
-  # item counts per phase
-  T = 1024
+  # item counts per phase (T: elements per tile, the plan's shape)
   nTF = -(-op.ktot // (T - 2 * ((msf * 5 + 2) & ~1)))
   nTA = -(-op.ktot // (T - 2 * ((msa * 5 + 1) & ~1)))
   phases = [(f"F{b}", b * nTF, (b + 1) * nTF) for b in range(nbF)]
   phases += [(f"A{b}", nbF * nTF + b * nTA, nbF * nTF + (b + 1) * nTA) for b in range(nbA)]
   summ = {"N": a.N, "K": a.K, "nsteps": a.nsteps, "blocks": [msf, msa], "items": int(items),
+          "tile_elements": int(T), "waves": int(waves),
           "sweep_us_untraced": t_plain, "sweep_us_traced": float(done.max()),
           "xcc_items": np.bincount(xcc, minlength=8).tolist(), "phases": {}}
   for name, lo, hi in phases:
@@ -86,8 +86,8 @@ def main():
   waiting = [int(((deq <= g) & (ready > g)).sum()) for g in grid]
   summ["timeline_5us"] = {"t": grid.tolist(), "in_flight": inflight, "waiting": waiting}
   os.makedirs(a.out, exist_ok=True)
-  np.save(os.path.join(a.out, f"trace_N{a.N}_f{msf}.npy"), t)
-  with open(os.path.join(a.out, f"trace_N{a.N}_f{msf}.json"), "w") as f:
+  np.save(os.path.join(a.out, f"trace_N{a.N}_f{msf}_w{waves}.npy"), t)
+  with open(os.path.join(a.out, f"trace_N{a.N}_f{msf}_w{waves}.json"), "w") as f:
     json.dump(summ, f, indent=1)
   print(json.dumps({k: v for k, v in summ.items() if k != "timeline_5us"}, indent=1))
   print("in flight every 20 us:", inflight[::4])
