@@ -99,13 +99,15 @@ def p_flops_per_update(Np):
 def halo_factor(T, H):
   """Lanes issued per useful lane of a tile of T elements whose launch writes T - 2 H."""
   return T / float(T - 2 * H)
-PROFILE_TRAFFIC = {  # per-launch PMC traffic of the sweep kernels (profiles/r04/collect.sh)
-    "jumps": os.path.join(ROOT, "profiles", "r04", "headline", "pmc_traffic.json"),
-    "snapshots": os.path.join(ROOT, "profiles", "r02", "pmc_traffic_snapshots.json"),
-    "p": os.path.join(ROOT, "profiles", "r04", "p", "pmc_traffic.json")}
-PROFILE_SQ = {  # SQ passes of the same benches: issued fp64 instructions of the dominant kernel
-    "jumps": os.path.join(ROOT, "profiles", "r04", "headline", "sq_summary.json"),
-    "p": os.path.join(ROOT, "profiles", "r04", "p", "sq_summary.json")}
+# Profiles of bench configurations (profiles/r04/collect.sh): each directory holds the per-launch
+# PMC traffic of the sweep kernel (pmc_traffic.json) and its SQ passes (sq_summary.json: issued
+# fp64 instructions); a bench line uses the one whose N, K, shape and kernel instantiation match
+PROFILE_DIRS = {
+    "jumps": [os.path.join(ROOT, "profiles", "r04", d)
+              for d in ("headline_w12", "N8_dflow", "N1", "headline")],
+    "snapshots": [os.path.join(ROOT, "profiles", "r02")],
+    "p": [os.path.join(ROOT, "profiles", "r04", "p")]}
+PROFILE_TRAFFIC_FILE = {"snapshots": "pmc_traffic_snapshots.json"}  # default pmc_traffic.json
 
 
 def parse(argv=None):
@@ -830,19 +832,22 @@ def main(argv=None):
            if pairs and dataflow else None)
   same_kernel = lambda names: kinst is None or any(  # noqa: E731
       str(n).startswith(kinst) for n in (names or []))
-  if os.path.exists(PROFILE_TRAFFIC[prof_key]):
+  prof_dir = None  # the matching profile directory (its SQ summary is read below)
+  for d in PROFILE_DIRS[prof_key]:
     try:
-      with open(PROFILE_TRAFFIC[prof_key]) as f:
+      with open(os.path.join(d, PROFILE_TRAFFIC_FILE.get(prof_key, "pmc_traffic.json"))) as f:
         tr = json.load(f)
-      if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
-          and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
-          and tr.get("record", "snapshots") == args.record
-          and tr.get("indicator", "jump") == args.indicator
-          and same_kernel(tr.get("adj_kernel"))):
-        traffic = tr.get("adj_bytes_per_launch")
-        traffic_src = tr.get("source")
     except (OSError, ValueError):
-      pass
+      continue
+    if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
+        and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
+        and tr.get("record", "snapshots") == args.record
+        and tr.get("indicator", "jump") == args.indicator
+        and same_kernel(tr.get("adj_kernel"))):
+      traffic = tr.get("adj_bytes_per_launch")
+      traffic_src = os.path.relpath(d, ROOT)
+      prof_dir = d
+      break
 
   # Jump record: the same launches priced with the snapshot sweep's algorithmic bytes (what
   # the snapshot algorithm moves for the same steps) -- an effective rate, not HBM traffic.
@@ -971,17 +976,17 @@ def main(argv=None):
   if pmode:
     out["prolong_us"] = float(np.mean(prolong_us))
     try:  # issued fp64 of k_adj_p from the SQ passes of the same bench (profiles/r04/p/)
-      with open(PROFILE_SQ["p"]) as fh:
+      with open(os.path.join(prof_dir, "sq_summary.json")) as fh:
         sq = json.load(fh)
-      if N == 4 and K == (1 << 20) and sweep.batch == 1 and traffic is not None:
+      if traffic is not None:
         f = out["roofline_fp64"]
         fl = sq["fp64_flops_issued_per_launch"]
         f["pmc_issued_per_launch"] = fl
         f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
         f["pmc_issued_over_useful"] = fl / (adj_fpu * upl)
         f["pmc_wait_any_frac"] = sq.get("wait_any_frac_of_wave_cycles")
-        f["pmc_source"] = os.path.relpath(PROFILE_SQ["p"], ROOT)
-    except (OSError, ValueError, KeyError):
+        f["pmc_source"] = os.path.relpath(os.path.join(prof_dir, "sq_summary.json"), ROOT)
+    except (OSError, ValueError, KeyError, TypeError):
       pass
   if dataflow:
     r = out["roofline"]
@@ -1002,20 +1007,19 @@ def main(argv=None):
     out["stream_copy"]["fwd_frac_of_achievable"] = None
     if out.get("roofline_effective"):
       out["roofline_effective"].update({"fwd_GBs": None, "fwd_frac": None})
-    # the PMC-measured issued fp64 flops of the same launch shape (SQ passes of this bench,
-    # profiles/r04/collect.sh), when N and K match
+    # the PMC-measured issued fp64 flops of the same launch (SQ passes of this bench,
+    # profiles/r04/collect.sh), from the profile whose traffic matched
     try:
-      with open(PROFILE_SQ["jumps"]) as fh:
+      with open(os.path.join(prof_dir, "sq_summary.json")) as fh:
         sq = json.load(fh)
-      if (N == 4 and K == (1 << 20) and sweep.batch == 1 and fchunks == [20]
-          and chunks == [10, 10] and same_kernel(sq.get("kernel"))):
+      if same_kernel(sq.get("kernel")):
         fl = sq["fp64_flops_issued_per_launch"]
         f["pmc_issued_per_launch"] = fl
         f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
         f["pmc_issued_over_useful"] = fl / ((fwd_fpu + adj_fpu) * Np * ktot * nsteps)
         f["pmc_wait_any_frac"] = sq.get("wait_any_frac_of_wave_cycles")
-        f["pmc_source"] = os.path.relpath(PROFILE_SQ["jumps"], ROOT)
-    except (OSError, ValueError, KeyError):
+        f["pmc_source"] = os.path.relpath(os.path.join(prof_dir, "sq_summary.json"), ROOT)
+    except (OSError, ValueError, KeyError, TypeError):
       pass
     out["dataflow"] = {"launches_per_sweep": 1, "blocks_fwd": fchunks, "blocks_adj": chunks,
                        "refine_in_launch": fused_refine,
