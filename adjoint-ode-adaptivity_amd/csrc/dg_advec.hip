@@ -1180,12 +1180,13 @@ bool sweep_shape(const dg_plan* p, int nsteps, int* waves, int* msf, int* msa) {
   } else {
     // as the record sweeps' tile width; on the 6-wave-per-SIMD uniform bodies (Np <= 5) 12-wave
     // tiles where their shape allows (1536 elements, 2 workgroups per CU; forward halo 1.15
-    // instead of 1.25, a third fewer items): +3-4 % at N = 4, +1-3 % at N = 2, equal at N = 1
+    // instead of 1.25, a third fewer items): +3-4 % at N = 4, +1-3 % at N = 2
     // (profiles/r04/take/, perN/, shape_ab/)
     nw = 4 * w;
     tiles = rec_fwd_width(p) == w && (w == 1 || w == 2);
-    if (tiles && w == 2 && p->uniform && p->NP <= 5 && p->sweep_lane_elems == 2 && f >= 10 &&
-        a == 10)
+    // (Np = 2 keeps 8 waves: at 8 waves per SIMD, four 8-wave groups per CU, see SweepOcc)
+    if (tiles && w == 2 && p->uniform && p->NP >= 3 && p->NP <= 5 && p->sweep_lane_elems == 2 &&
+        f >= 10 && a == 10)
       nw = 12;
   }
   *msf = f;

@@ -162,13 +162,19 @@ __device__ __forceinline__ uint64_t ld8_agent(const void* p) {
 // the loops (the edge tiles' prologue, the indicator's partial-row combine).  Np = 6 spills
 // inside a loop at 80, and the non-uniform bodies (the metric per element) spill more: they
 // keep the unconstrained count.  (Np 2, 3 fit 6 waves unconstrained.)
-template <int NP, bool UNI> struct SweepOcc {
-  static constexpr int waves_per_simd = (UNI && NP <= 5) ? 6 : 1;  // 1: no constraint
+// At Np = 2 the bodies fit 8 waves per SIMD by VGPRs (57) but not by SGPRs: 99 SGPRs admit 6
+// (MI355X_MICROARCH.md, residency: floor(800 / (ceil(sgpr/16)*16 + 16))).  Asked for 8, the
+// compiler keeps 78 SGPRs and 58 VGPRs without spilling, and 4- or 8-wave workgroups then fill
+// 32 wave slots per CU: N = 1 +4-6 % (6.09 / 6.17e11 against 5.88 / 5.79e11 for the 12-wave
+// default, profiles/r04/wpe8/).  Np = 3 spills 28 B per lane at 8 and gains nothing.
+template <int NP, bool UNI, int NW = 8> struct SweepOcc {
+  static constexpr int waves_per_simd =
+      (UNI && NP == 2 && (NW == 4 || NW == 8)) ? 8 : (UNI && NP <= 5) ? 6 : 1;  // 1: none
 };
 
 template <int NP, bool UNI, int NW, int MSF, int MSA, int E>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
-    E == 2 ? SweepOcc<NP, UNI>::waves_per_simd : 1))) void k_sweep_rp(SweepArgs<NP, MSF> a) {
+    E == 2 ? SweepOcc<NP, UNI, NW>::waves_per_simd : 1))) void k_sweep_rp(SweepArgs<NP, MSF> a) {
   using G = RpGeo<NP, NW, E>;
   constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
   constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;

@@ -104,7 +104,7 @@ def halo_factor(T, H):
 # fp64 instructions); a bench line uses the one whose N, K, shape and kernel instantiation match
 PROFILE_DIRS = {
     "jumps": [os.path.join(ROOT, "profiles", "r04", d)
-              for d in ("headline_w12", "N8_dflow", "N1", "headline")],
+              for d in ("headline_w12", "N8_dflow", "N1_w8", "N1", "headline")],
     "snapshots": [os.path.join(ROOT, "profiles", "r02")],
     "p": [os.path.join(ROOT, "profiles", "r04", "p")]}
 PROFILE_TRAFFIC_FILE = {"snapshots": "pmc_traffic_snapshots.json"}  # default pmc_traffic.json

@@ -118,7 +118,7 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             width 2, else 4); a sweep is chunked by halving
  *   DG_TUNE_SWEEP_WAVES       workgroup waves of the dataflow sweep (dg_lserk4_sweep_rec): 0 (the
  *                             default: as the record sweeps' tile width, 4 or 8 waves, except
- *                             12 on uniform meshes at Np <= 5 with 1024-element record tiles,
+ *                             12 on uniform meshes at 3 <= Np <= 5 with 1024-element record tiles,
  *                             >= 10-step forward and 10-step adjoint blocks, and 8 on uniform
  *                             meshes at Np = 9), 4, 8, 12 or 16 (16 at
  *                             Np <= 5); tiles of 128 * waves elements in both directions, also
