@@ -28,6 +28,7 @@ DG_TUNE_SWEEP_SPIN_LIMIT = 13
 DG_TUNE_SWEEP_WAVES = 14
 DG_TUNE_SWEEP_LANE_ELEMENTS = 15
 DG_TUNE_SWEEP_TAKE = 16
+DG_TUNE_SWEEP_EXCHANGE = 17
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
@@ -72,6 +73,7 @@ SIGNATURES = {
                                       ctypes.c_double, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "dg_plan_query_sweep": (_i32, [_vp, _i32, _vp]),
     "dg_plan_query_sweep_ex": (_i32, [_vp, _i32, _vp]),
+    "dg_plan_query_sweep_kernel": (_i32, [_vp, _i32, _vp]),
     "dg_sweep_status": (_i32, [_vp, ctypes.POINTER(_i32), _vp]),
     "dg_plan_sweep_trace": (_i32, [_vp, _vp]),
     "dg_plan_query_p": (_i32, [_vp, _vp]),

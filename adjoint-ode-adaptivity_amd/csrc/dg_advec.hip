@@ -1193,9 +1193,13 @@ bool sweep_shape(const dg_plan* p, int nsteps, int* waves, int* msf, int* msa) {
   *msa = a;
   *waves = nw;
   tiles = tiles && (p->sweep_lane_elems == 2 || (p->NP <= 3 && (nw == 4 || nw == 8)));
-  const int T = 64 * p->sweep_lane_elems * nw;  // elements per tile
+  if (p->sweep_exchange == 1)  // overlapped waves: pairs on 8, 12 or 16 (Np <= 5) waves, 20- or
+                               // 10-step forward and 10-step adjoint blocks
+    tiles = tiles && p->sweep_lane_elems == 2 &&
+            (nw == 8 || nw == 12 || (nw == 16 && p->NP <= 5)) && f >= 10 && a == 10;
+  const int T = sweep_tile_elems(p, nw);  // elements per tile
   return p->rec_sweep && rec_pairs(p) && tiles &&
-         (f == 5 || f == 10 || (f == 20 && T >= 1024)) && (a == 5 || a == 10) && nsteps > 0 &&
+         (f == 5 || f == 10 || (f == 20 && T >= 900)) && (a == 5 || a == 10) && nsteps > 0 &&
          nsteps % f == 0 && nsteps % a == 0 && nsteps <= sweep_max_steps();
 }
 
@@ -1374,9 +1378,9 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     const int k = std::atoi(v);
     if (k == 2 || (k == 4 && p->NP <= 3)) p->sweep_lane_elems = k;
   }
-  if (const char* v = std::getenv("DG_SWEEP_TAKE")) {
+  if (const char* v = std::getenv("DG_SWEEP_EXCHANGE")) {
     const int k = std::atoi(v);
-    if (k == 0 || k == 1) p->sweep_take = k;
+    if (k == 0 || k == 1) p->sweep_exchange = k;
   }
   if (const char* v = std::getenv("DG_SWEEP_WAVES")) {
     const int k = std::atoi(v);
@@ -1505,8 +1509,9 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       p->rec_lane_elems = int(value);
       return DG_OK;
     case DG_TUNE_SWEEP_WAVES:
-      if (!(value == 0 || value == 4 || value == 8 || value == 12 || value == 16))
-        return fail(DG_ERR_ARG, "sweep waves: 0 (as the record tile width), 4, 8, 12 or 16");
+      if (!(value == 0 || value == 4 || value == 8 || value == 12 || (value == 16 && p->NP <= 5)))
+        return fail(DG_ERR_ARG, "sweep waves: 0 (as the record tile width), 4, 8, 12 or 16 "
+                                "(16 at Np <= 5)");
       p->sweep_waves = int(value);
       return DG_OK;
     case DG_TUNE_SWEEP_LANE_ELEMENTS:
@@ -1515,8 +1520,14 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       p->sweep_lane_elems = int(value);
       return DG_OK;
     case DG_TUNE_SWEEP_TAKE:
-      if (value != 0 && value != 1) return fail(DG_ERR_ARG, "sweep take: 0 (counter) or 1 (workgroup id)");
-      p->sweep_take = int(value);
+      // removed in round 5 (item = workgroup id relied on in-order dispatch per XCD): only the
+      // take counter (0) remains
+      if (value != 0) return fail(DG_ERR_ARG, "sweep take: only 0 (the take counter) is supported");
+      return DG_OK;
+    case DG_TUNE_SWEEP_EXCHANGE:
+      if (value != 0 && value != 1)
+        return fail(DG_ERR_ARG, "sweep exchange: 0 (LDS + barrier per level) or 1 (overlapped waves)");
+      p->sweep_exchange = int(value);
       return DG_OK;
     case DG_TUNE_SWEEP_SPIN_LIMIT:
       if (value < 0 || value > (1 << 30)) return fail(DG_ERR_ARG, "spin limit: 0 (default) .. 2^30");
@@ -1601,6 +1612,11 @@ int dg_plan_reserve(dg_plan* p, int64_t K_capacity) {
   }
   HIP_TRY(hipMemcpy(sc, p->d_scale, sizeof(double) * p->K, hipMemcpyDeviceToDevice));
   HIP_TRY(hipMemcpy(vx, p->d_VX, sizeof(double) * (p->K + 1), hipMemcpyDeviceToDevice));
+  // A safe point (the device is idle): the dataflow scratch regions a grown scratch retired go
+  // now.  Like the plan's own scratch fields below, they may be held by a HIP graph captured
+  // before this call: such graphs must be re-captured after a reserve (include/dg_advec.h).
+  for (void* r : p->sweep_retired) (void)hipFree(r);
+  p->sweep_retired.clear();
   (void)hipFree(p->d_scale);
   (void)hipFree(p->d_VX);
   (void)hipFree(p->d_scratch);
@@ -1878,7 +1894,8 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
     if (!fin && term) fin = w;
     if (!fin) {
       char* data = nullptr;
-      if (const int rc = sweep_scratch(p, 256, fbytes, st, &data)) return rc;
+      const size_t fcap = sizeof(double) * size_t(p->K_cap * p->batch) * size_t(p->NP);
+      if (const int rc = sweep_scratch(p, 256, fcap, st, &data)) return rc;
       fin = reinterpret_cast<double*>(data);
     }
     if (const int rc = dg_lserk4_fwd_rec(p, u0, fin, t0, dt, nsteps, jumps, stream)) return rc;
@@ -1901,7 +1918,13 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   }
   const int nbF = nsteps / msf, nbA = nsteps / msa;
   const int64_t items = sweep_items(p, waves, msf, msa, nsteps);
-  const size_t sync_bytes = (sizeof(uint32_t) * size_t(sweep_sync_words() + items) + 255) & ~size_t(255);
+  // The scratch is sized for the plan's reserved capacity (K_cap elements per trajectory), so
+  // the refines of an adapt loop within it (dg_plan_refine: ktot += batch) reuse one region
+  // instead of retiring a slightly smaller one per iteration.
+  const int64_t kcap = p->K_cap * p->batch;
+  const int64_t items_cap = sweep_items(p, waves, msf, msa, nsteps, kcap);
+  const size_t sync_bytes = (sizeof(uint32_t) * size_t(sweep_sync_words() + items_cap) + 255) &
+                            ~size_t(255);
   // fields: forward block outputs U[1..nbF-1] (+ U[nbF] unless the caller keeps u^N), adjoint
   // block outputs W[1..nbA-1] (+ a copy of the caller's terminal weight when one block would
   // read and write w); partial indicator rows for nbA - 1 blocks
@@ -1909,13 +1932,16 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   const int nfields = (nbF - 1) + (uN ? 0 : 1) + (nbA - 1) + wcopy;
   const int nparts = eta ? nbA - 1 : 0;
   const int64_t am_parts = idx ? sweep_tiles_adj(p, waves, msa) : 0;
-  const size_t bytes = sync_bytes + fbytes * size_t(nfields) +
-                       sizeof(double) * size_t(p->ktot) * size_t(nparts) + 16 * size_t(am_parts);
+  const int64_t am_parts_cap = idx ? sweep_tiles_adj(p, waves, msa, kcap) : 0;
+  const size_t fcap = sizeof(double) * size_t(kcap) * size_t(p->NP);
+  const size_t data_bytes = fcap * size_t(nfields) + sizeof(double) * size_t(kcap) * size_t(nparts) +
+                            16 * size_t(am_parts_cap);
   char* data = nullptr;
-  if (const int rc = sweep_scratch(p, sync_bytes, bytes - sync_bytes, st, &data)) return rc;
+  if (const int rc = sweep_scratch(p, sync_bytes, data_bytes, st, &data)) return rc;
   const uint64_t sig = uint64_t(items) * 1000003u ^ (uint64_t(waves) << 56) ^
+                      (uint64_t(p->sweep_exchange) << 61) ^
                       (uint64_t(msf) << 48) ^ (uint64_t(msa) << 40) ^ (uint64_t(nsteps) << 32) ^
-                      uint64_t(sweep_tiles_adj(p, waves, msa)) ^ (uint64_t(p->sweep_take) << 62);
+                      uint64_t(sweep_tiles_adj(p, waves, msa));
   if (p->sweep_items != items || p->sweep_sig != sig) {
     // the take counter numbers launches by items per launch and the fused refine's arrival
     // counter by the last block's tiles: a new shape starts both afresh
@@ -1951,7 +1977,6 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
   b.am_pi = idx ? reinterpret_cast<int64_t*>(am + am_parts) : nullptr;
   b.err_host = p->d_sweep_err;
   b.spin_limit = p->sweep_spin_limit;
-  b.take = p->sweep_take;
   const int mode = eta ? (kEtaOn | ((aflags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
                           ((aflags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
                        : 0;
@@ -2003,7 +2028,24 @@ int dg_plan_query_sweep_ex(const dg_plan* p, int nsteps, int64_t out[6]) {
   out[2] = msa;
   out[3] = on ? sweep_items(p, waves, msf, msa, nsteps) : 0;
   out[4] = waves;
-  out[5] = 64 * int64_t(p->sweep_lane_elems) * waves;
+  out[5] = sweep_tile_elems(p, waves);
+  return DG_OK;
+}
+
+int dg_plan_query_sweep_kernel(const dg_plan* p, int nsteps, int64_t out[8]) {
+  if (!p || !out) return fail(DG_ERR_ARG, "null argument");
+  int waves = 0, msf = 0, msa = 0;
+  const bool on = sweep_shape(p, nsteps, &waves, &msf, &msa);
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+  if (!on) return DG_OK;
+  out[0] = p->NP;
+  out[1] = p->uniform ? 1 : 0;
+  out[2] = waves;
+  out[3] = msf;
+  out[4] = msa;
+  out[5] = p->sweep_lane_elems;
+  out[6] = p->sweep_exchange;
+  out[7] = sweep_waves_per_simd(p, waves);
   return DG_OK;
 }
 

@@ -487,9 +487,10 @@ struct dg_plan {
   // consecutive elements per lane of the dataflow sweep's tiles: 2 (pair tiles), or 4 at
   // Np <= 3 on 4- or 8-wave workgroups (tiles of 64 * 4 * waves elements)
   int sweep_lane_elems = 2;
-  // how a dataflow workgroup gets its item: 0 the take counter, 1 its workgroup id (the
-  // epoch from the item's own flag)
-  int sweep_take = 0;
+  // how the dataflow sweep's tiles exchange faces: 0 through LDS with a workgroup barrier per
+  // Horner level (dg_rec_tiles.h), 1 overlapped waves: DPP within a wave, one LDS exchange and
+  // barrier per step (dg_ovl_tiles.h)
+  int sweep_exchange = 0;
   uint64_t* sweep_trace = nullptr;  // dg_plan_sweep_trace: per-item timestamps (profiling)
   int cu_count = 0;  // compute units of the plan's device (the dataflow grid)
   int xcd_order = 1;  // XCD-aware tile order
@@ -640,10 +641,13 @@ struct SweepBufs {
   int64_t* am_pi;
   uint32_t* err_host;  // nullable: the plan's host-visible watchdog flag (d_sweep_err)
   int32_t spin_limit;  // 0: the default
-  int32_t take;        // dg_plan::sweep_take
 };
-int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps);
-int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa);
+int sweep_tile_elems(const dg_plan* p, int waves);
+int sweep_waves_per_simd(const dg_plan* p, int waves);  // the kernel's occupancy target (0: none)
+// work items / last-block adjoint tiles of a dataflow sweep over the plan's ktot elements, or
+// over `elems` (>= 0: the scratch sizing for the reserved capacity)
+int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps, int64_t elems = -1);
+int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa, int64_t elems = -1);
 int sweep_launch_rec(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,
                      double dt, int nsteps, int mode, hipStream_t st);
 int sweep_sync_words();

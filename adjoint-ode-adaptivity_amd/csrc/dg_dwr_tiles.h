@@ -1,0 +1,379 @@
+// dg_dwr_tiles.h — the p-enriched DWR estimate's reverse steps in Horner form (round 5).
+// Internal to libdgadv.so; included by dg_dwr.hip.
+//
+// Per reverse step n (dg_dwr.hip, "k_adj_p"): prolong the order-N snapshot u^n to order N+1
+// (v = P u^n), recompute S_{N+1}(v), pair the residual R^n = P u^{n+1} - S_{N+1}(v) with the
+// order-(N+1) adjoint w^{n+1} (eta -= w^{n+1} . R^n), then w^n = S_{N+1}^T w^{n+1}.  Round 3
+// ran both S and S^T as the five low-storage stages (utils/One_code.mlx:120-137).  Here both
+// are the LSERK4 step's stability polynomial in Horner form (dg_rec_tiles.h "Horner form"):
+//   S(v)    = v + Z_{b0}(t),  t = v + Z_{b1}(t'), ...,  t'' = beta_4 v + beta_5 Z_{b4/beta5}(v)
+//   S^T w   = w + z^T t,      t = w + z^T t', ...,     t'' = beta_4 w + beta_5 z^T w
+// five applications of the order-(N+1) operator each way (one face exchange each), with no
+// low-storage carry: at Np = 6 about 290 + 300 fp64 operations per element and step instead
+// of the stage loop's 368 + 360.  The prolongation (even/odd blocks), the residual pairing,
+// the tile layout (one element per lane, snapshot tiles prefetched into registers a step
+// ahead and committed to LDS behind the forward levels' barriers), the halo (5 per step) and
+// the outputs are round 3's.  The order-(N+1) operator and prolongation blocks are re-read
+// from the kernel-argument segment where they are used (OpSrc, dg_rec_tiles.h): together they
+// are 39 doubles at Np = 6, which held as arguments spilled SGPRs into VGPR lanes.
+// Sources: matlab/MAIN.m:32-34 (adjoint at order Ns+1), matlab/adj_march.m:103-117 (err(k) =
+// v_k' R_k), python/Main_finite_difference.py:79-94 (errEst); DESIGN.md §6c.
+#pragma once
+#include "dg_rec_tiles.h"
+
+namespace dgk {
+
+// Prolongation in even/odd coordinates: e_hi = Pe e_lo, o_hi = Po o_lo.
+template <int NPL> struct PrEO {
+  static constexpr int NPH = NPL + 1;
+  static constexpr int NEL = (NPL + 1) / 2, NOL = NPL / 2;
+  static constexpr int NEH = (NPH + 1) / 2, NOH = NPH / 2;
+  double Pe[NEH * NEL];
+  double Po[NOH * NOL];
+};
+
+// The Horner-form estimate's launch arguments (MS reverse steps n0+MS-1 .. n0).  op: the
+// order-(N+1) operator, folded, dt*2/h folded on uniform meshes; bnd[5 st + l]: the inflow
+// weights of level l of step n0+st's forward recompute (rp_block_bnd: b_4/beta_5, b_3, b_2,
+// b_1, b_0), then one 0.
+template <int NPL, int MS> struct AdjPHArgs {
+  EOArgs<NPL + 1> op;
+  PrEO<NPL> pr;
+  double sc;        // dt (non-uniform meshes multiply by scale[k])
+  double beta[6];   // the stability polynomial's coefficients (rk_poly)
+  double bnd[MS * 5 + 1];
+  int64_t ktot;
+  int64_t stride;   // doubles between consecutive order-N snapshots
+  int32_t K;
+  int32_t has_eta;  // kEta* bits
+  int32_t xcd;
+};
+
+template <int NPL, class PR>
+__device__ __forceinline__ void prolong_eo(const double* __restrict__ u, const PR& pr,
+                                           double* ev, double* od) {
+  using R = PrEO<NPL>;
+  double el[R::NEL], ol[R::NOL];
+  to_eo<NPL>(u, el, ol);
+#pragma unroll
+  for (int k = 0; k < R::NEH; ++k) {
+    double t = pr.Pe[k * R::NEL] * el[0];
+#pragma unroll
+    for (int j = 1; j < R::NEL; ++j) t = fma(pr.Pe[k * R::NEL + j], el[j], t);
+    ev[k] = t;
+  }
+#pragma unroll
+  for (int k = 0; k < R::NOH; ++k) {
+    double t = pr.Po[k * R::NOL] * ol[0];
+#pragma unroll
+    for (int j = 1; j < R::NOL; ++j) t = fma(pr.Po[k * R::NOL + j], ol[j], t);
+    od[k] = t;
+  }
+}
+
+// A kernel-argument block read where it is used (dgr::OpSrc's technique for any block).
+template <class T> struct KaSrc {
+  const DG_KAS T* p;
+  __device__ __forceinline__ const DG_KAS T& get() const {
+    const DG_KAS T* q = p;
+    asm volatile("" : "+s"(q));
+    return *q;
+  }
+};
+
+template <int NPL, int W> struct PHGeo {
+  static constexpr int NPH = NPL + 1;
+  static constexpr int LB = kBlock * W, T = LB;
+  static constexpr int kImgD = T * NPH + 2;  // the image holds the w tile or a snapshot tile
+  static constexpr int kFB = (kImgD + 1) & ~1;
+  static constexpr int kFaceD = 4 * (T + 2);  // two double-buffered face arrays, padded by 1
+  static constexpr int kLds = kFB + kFaceD;
+};
+
+// One tile of a Horner-form estimate launch.  snap = u^{n0}; reads u^{n0} .. u^{n0+MS}.
+// `ka`: the argument block in the kernarg segment (operator and prolongation reads); `kbnd`:
+// its bnd array there (the edge tiles' lane-indexed reads).
+template <int NPL, bool UNI, int W, int MS, bool EDGE>
+__device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t tile,
+                                           const double* __restrict__ win,
+                                           double* __restrict__ wout,
+                                           const double* __restrict__ snap,
+                                           double* __restrict__ eta,
+                                           const double* __restrict__ scale,
+                                           const AdjPHArgs<NPL, MS>& args,
+                                           const DG_KAS AdjPHArgs<NPL, MS>* ka,
+                                           const double* kbnd) {
+  constexpr int NPH = NPL + 1;
+  using G = PHGeo<NPL, W>;
+  using A = AdjPHArgs<NPL, MS>;
+  constexpr int T = G::T, LB = G::LB;
+  // the reverse cone is 5 elements per step; the forward recompute of a step needs 5 more
+  // around the output elements, which the halo of the steps still to come covers
+  constexpr int H = MS * 5;
+  constexpr int TE = T - 2 * H;
+  static_assert(TE % 2 == 0 && TE > 0, "tile output must be 16-byte aligned");
+  constexpr int NE = EOArgs<NPH>::NE, NO = EOArgs<NPH>::NO, NH = NPH - 1;
+  const KaSrc<EOArgs<NPH>> os{reinterpret_cast<const DG_KAS EOArgs<NPH>*>(
+      reinterpret_cast<const DG_KAS char*>(ka) + offsetof(A, op))};
+  const KaSrc<PrEO<NPL>> ps{reinterpret_cast<const DG_KAS PrEO<NPL>*>(
+      reinterpret_cast<const DG_KAS char*>(ka) + offsetof(A, pr))};
+  const int lane = threadIdx.x;
+  const int64_t e0 = tile * TE - H;
+  const int64_t ndh = args.ktot * NPH, ndl = args.ktot * NPL;
+  constexpr int CB = G::kLds;  // lds[CB + 5 st + l]: level inflow weights; lds[CB + 5 MS] = 0
+
+  TileRegs<NPH, W> pw;
+  TileRegs<NPL, W> pa, pb;
+  tile_issue<NPH, W, EDGE>(win, e0, ndh, pw);
+  tile_issue<NPL, W, EDGE>(snap + MS * args.stride, e0, ndl, pa);
+  tile_issue<NPL, W, EDGE>(snap + (MS - 1) * args.stride, e0, ndl, pb);
+  tile_commit<NPH, W>(pw, lds);
+  if constexpr (EDGE) {
+    if (lane <= MS * 5) lds[CB + lane] = kbnd[lane];  // lane-indexed: from the kernarg segment
+  }
+  __syncthreads();
+  double we[NE], wo[NO];  // the order-(N+1) adjoint in dual even/odd coordinates
+  {
+    const double* w = lds + pw.off + lane * NPH;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) {
+      we[k] = w[k] + w[NH - k];
+      wo[k] = w[k] - w[NH - k];
+    }
+    if constexpr (NE > NO) we[NO] = w[NO];
+  }
+  const Elem E = elem_info<H, T, EDGE>(e0, lane, args.ktot, args.K);
+  double sc = args.sc;
+  if constexpr (!UNI) sc *= E.inrange ? scale[E.kl] : 0.0;
+  __syncthreads();  // the w image is read
+  tile_commit<NPL, W>(pa, lds);
+  __syncthreads();
+  double ne[NE], no[NO];  // P u^{n+1} of this lane's element
+  prolong_eo<NPL>(lds + pa.off + lane * NPL, ps.get(), ne, no);
+  __syncthreads();
+  tile_commit<NPL, W>(pb, lds);
+  int off = pb.off;
+  __syncthreads();
+  double eacc = 0.0;
+  const double b4 = args.beta[4], b5 = args.beta[5], b3 = args.beta[3], b2 = args.beta[2];
+
+#pragma unroll 1
+  for (int st = MS - 1; st >= 0; --st) {
+    // ---- v = P u^n, and the next snapshot's loads in flight behind this step ----
+    double ve[NE], vo[NO];
+    prolong_eo<NPL>(lds + off + lane * NPL, ps.get(), ve, vo);
+    if (st > 0) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
+
+    // ---- S_{N+1}(v) by Horner (rp_step_tile's level arithmetic at order N+1) ----
+    double te[NE], to[NO];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+      const int fL = G::kFB + (l & 1) * 2 * (T + 2), fR = fL + (T + 2);
+      {
+        const double e = (l == 0) ? ve[0] : te[0], o = (l == 0) ? vo[0] : to[0];
+        lds[fL + lane + 1] = e + o;
+        lds[fR + lane + 1] = e - o;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      double pe[NE], po[NO];
+      {
+        const auto& op = os.get();
+        const double* xo = (l == 0) ? vo : to;
+        const double* xe = (l == 0) ? ve : te;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          double a;
+          int j0 = 0;
+          if (UNI && l >= 3) {
+            a = ve[k];
+          } else if (UNI && l >= 1) {
+            a = (l == 1 ? b3 : b2) * ve[k];
+          } else {
+            a = op.Qeo[k * NO] * xo[0];
+            j0 = 1;
+          }
+#pragma unroll
+          for (int j = j0; j < NO; ++j) a = fma(op.Qeo[k * NO + j], xo[j], a);
+          pe[k] = a;
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          double a;
+          int j0 = 0;
+          if (UNI && l >= 3) {
+            a = vo[k];
+          } else if (UNI && l >= 1) {
+            a = (l == 1 ? b3 : b2) * vo[k];
+          } else {
+            a = op.Qoe[k * NE] * xe[0];
+            j0 = 1;
+          }
+#pragma unroll
+          for (int j = j0; j < NE; ++j) a = fma(op.Qoe[k * NE + j], xe[j], a);
+          po[k] = a;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NE; ++k) pin(pe[k]);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) pin(po[k]);
+      __syncthreads();
+      // a trajectory's first element reads the level's inflow weight, its last one its own
+      // right node (index selection: dg_common.h)
+      const int iL = EDGE && E.first ? CB + st * 5 + l : fR + lane;
+      const int iR = EDGE && E.last ? fR + lane + 1 : fL + lane + 2;
+      const double vL = lds[iL], vR = lds[iR];
+      const double dlt = vR - vL, sig = -(vL + vR);
+      const auto& ol = os.get();
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        const double z = fma(ol.le[k], dlt, pe[k]);
+        if constexpr (UNI) {
+          if (l == 0) te[k] = fma(b5, z, b4 * ve[k]);
+          else te[k] = z;  // level 4: S itself
+        } else {
+          if (l == 0) te[k] = fma(b5 * sc, z, b4 * ve[k]);
+          else if (l < 3) te[k] = fma(sc, z, (l == 1 ? b3 : b2) * ve[k]);
+          else te[k] = fma(sc, z, ve[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        const double z = fma(ol.lo[k], sig, po[k]);
+        if constexpr (UNI) {
+          if (l == 0) to[k] = fma(b5, z, b4 * vo[k]);
+          else to[k] = z;
+        } else {
+          if (l == 0) to[k] = fma(b5 * sc, z, b4 * vo[k]);
+          else if (l < 3) to[k] = fma(sc, z, (l == 1 ? b3 : b2) * vo[k]);
+          else to[k] = fma(sc, z, vo[k]);
+        }
+      }
+    }
+
+    // ---- eta -= w^{n+1} . (P u^{n+1} - S_{N+1}(P u^n)) in dual x primal even/odd ----
+    if (args.has_eta) {
+      double c = 0.0;
+#pragma unroll
+      for (int k = 0; k < NE; ++k) c = fma(we[k], ne[k] - te[k], c);
+#pragma unroll
+      for (int k = 0; k < NO; ++k) c = fma(wo[k], no[k] - to[k], c);
+      eacc -= c;
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) ne[k] = ve[k];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) no[k] = vo[k];
+    // the image's readers (the prolongation above) are 5 level barriers behind
+    if (st > 0) {
+      tile_commit<NPL, W>(pa, lds);
+      off = pa.off;
+    }
+
+    // ---- w^n = S_{N+1}^T w^{n+1} by Horner (rp_adj_tile's level arithmetic at order N+1) ----
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+      const int f0 = G::kFB + ((l + 1) & 1) * 2 * (T + 2), f1 = f0 + (T + 2);
+      double qe[NE], qo[NO], gd = 0.0, gs = 0.0;
+      {
+        const auto& op = os.get();
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+          const double v = (l == 0) ? we[k] : te[k];
+          qe[k] = UNI ? v : sc * v;
+          gd = fma(op.le[k], qe[k], gd);
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) {
+          const double v = (l == 0) ? wo[k] : to[k];
+          qo[k] = UNI ? v : sc * v;
+          gs = fma(op.lo[k], qo[k], gs);
+        }
+      }
+      const double g0 = gd + gs, g1 = gs - gd;
+      lds[f0 + lane + 1] = g0;
+      lds[f1 + lane + 1] = g1;
+      __builtin_amdgcn_sched_barrier(0);
+      double ae[NE], ao[NO];
+      {
+        const auto& op = os.get();
+#pragma unroll
+        for (int j = 0; j < NO; ++j) {
+          double t;
+          int k0 = 0;
+          if (l >= 3) {
+            t = wo[j];
+          } else if (l >= 1) {
+            t = (l == 1 ? b3 : b2) * wo[j];
+          } else {
+            t = op.Qeo[j] * qe[0];
+            k0 = 1;
+          }
+#pragma unroll
+          for (int k = k0; k < NE; ++k) t = fma(op.Qeo[k * NO + j], qe[k], t);
+          ao[j] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NO; ++k) pin(ao[k]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        const auto& op = os.get();
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+          double t;
+          int k0 = 0;
+          if (l >= 3) {
+            t = we[j];
+          } else if (l >= 1) {
+            t = (l == 1 ? b3 : b2) * we[j];
+          } else {
+            t = op.Qoe[j] * qo[0];
+            k0 = 1;
+          }
+#pragma unroll
+          for (int k = k0; k < NO; ++k) t = fma(op.Qoe[k * NE + j], qo[k], t);
+          ae[j] = t;
+        }
+#pragma unroll
+        for (int k = 0; k < NE; ++k) pin(ae[k]);
+      }
+      __syncthreads();
+      // nothing arrives at a trajectory's first element from the left (its uL is the
+      // inflow); its last element's uR is its own u_N (du1 = 0)
+      const double gl = lds[EDGE && E.first ? CB + MS * 5 : f1 + lane];
+      const double gr = lds[EDGE && E.last ? f1 + lane + 1 : f0 + lane + 2];
+      ae[0] -= gl + gr;
+      ao[0] += gr - gl;
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        if (l == 0) te[k] = fma(b5, ae[k], b4 * we[k]);
+        else if (l < 4) te[k] = ae[k];
+        else we[k] = ae[k];
+      }
+#pragma unroll
+      for (int k = 0; k < NO; ++k) {
+        if (l == 0) to[k] = fma(b5, ao[k], b4 * wo[k]);
+        else if (l < 4) to[k] = ao[k];
+        else wo[k] = ao[k];
+      }
+    }
+  }
+
+  if (args.has_eta && E.valid) eta_update(eta, E.e, eacc, args.has_eta);
+  {
+    const double(*pwe)[NE] = &we;
+    const double(*pwo)[NO] = &wo;
+    stage_out<NPH, W, H>(lds, pwe, pwo, true);  // the image's last reads are 5 barriers behind
+  }
+  __syncthreads();
+  const int64_t o0 = tile * TE * NPH;
+  if constexpr (EDGE) {
+    const int64_t rem = ndh - o0;
+    store_run<LB>(wout, o0, rem < int64_t(TE) * NPH ? rem : int64_t(TE) * NPH, lds);
+  } else {
+    store_full<TE * NPH, LB>(wout, o0, lds);
+  }
+}
+
+}  // namespace dgk

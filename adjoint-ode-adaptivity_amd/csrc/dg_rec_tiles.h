@@ -80,12 +80,12 @@ __device__ __forceinline__ double wt_ld8(__amdgpu_buffer_rsrc_t r, uint32_t off)
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kSc1));
 }
 
-// Coalesced 16-byte loads of the tile image [e0, e0 + T) (zeros outside [0, nd)), issued
-// together, then written to LDS.  Returns the image's offset (0 or 1 double).
-template <int NP, int NW, int E, bool EDGE, bool WT>
-__device__ __forceinline__ int rp_load(const double* __restrict__ g, int64_t e0, int64_t nd,
-                                       double* __restrict__ lds) {
-  using G = RpGeo<NP, NW, E>;
+// Coalesced 16-byte loads of the tile image [e0, e0 + G::T) (zeros outside [0, nd)), issued
+// together, then written to LDS.  Returns the image's offset (0 or 1 double).  G: the tile
+// geometry (G::T elements, G::LB lanes, G::kVec double2 per lane).
+template <class G, int NP, bool EDGE, bool WT>
+__device__ __forceinline__ int tile_load(const double* __restrict__ g, int64_t e0, int64_t nd,
+                                         double* __restrict__ lds) {
   const int64_t d0 = e0 * NP;
   const int64_t base = d0 & ~int64_t(1);
   const int off = int(d0 - base);
@@ -123,6 +123,12 @@ __device__ __forceinline__ int rp_load(const double* __restrict__ g, int64_t e0,
     if (v < nvec) *reinterpret_cast<double2*>(&lds[2 * v]) = rv[q];
   }
   return off;
+}
+
+template <int NP, int NW, int E, bool EDGE, bool WT>
+__device__ __forceinline__ int rp_load(const double* __restrict__ g, int64_t e0, int64_t nd,
+                                       double* __restrict__ lds) {
+  return tile_load<RpGeo<NP, NW, E>, NP, EDGE, WT>(g, e0, nd, lds);
 }
 
 // Store `count` doubles from lds[0..count) to g[o0..o0+count) (o0 even), write-through.

@@ -1,447 +1,16 @@
-// dg_sweep.hip — the jump-record sweep pair as ONE dataflow launch (dg_lserk4_sweep_rec).
-//
-// The launch-per-block sweep (dg_lserk4_fwd_rec + dg_lserk4_adj_rec, dg_rec.hip) runs three
-// launches per 20-step sweep at the default shape (forward 20, adjoint 10 + 10), and each
-// launch pays a fill (the first round of workgroups loading their tiles with nothing to
-// overlap) and a drain (the last round running partly empty: at K = 2^20 the forward's 1,279
-// tiles are 1.66 rounds of the 768 resident workgroups).  Here the same tile bodies
-// (dg_rec_tiles.h, policy WT = write-through hand-offs) are the work items of ONE launch:
-//   items, in queue order: forward block 0 tiles 0..nTF-1, forward block 1 tiles, ...,
-//   adjoint block 0 tiles 0..nTA-1 (reverse steps nsteps-MSA..nsteps-1), adjoint block 1, ...
-//   The grid has one workgroup per item; each takes the next item from one counter when the
-//   hardware starts it (not by blockIdx), so items start in queue order.  An item waits only
-//   for items earlier in the queue -- the previous block's tiles whose output ranges its
-//   input range (tile + halo) touches; the first adjoint block for the last forward block's
-//   tiles covering its range (whose completion implies every earlier forward block's records
-//   there) -- so the sweep cannot deadlock at any residency: the earliest waiting item's
-//   producers were taken before it by workgroups that are running and wait on nothing later.
-//   (A persistent grid looping over items measured 143 VGPRs: the compiler keeps both
-//   bodies' constants live across the loop; one item per workgroup keeps the registers of
-//   the separate kernels.)
-// Hand-offs (cdna_hip_programming.md §6 Guideline 16, R1; MI355X_MICROARCH.md, visibility):
-//   producer: every store of handed-off bytes (block states, the record, indicator partials)
-//     is write-through (`sc1`); every wave drains (`s_waitcnt vmcnt(0)`), a workgroup barrier,
-//     then one lane stores the item's flag (an agent-scope atomic store of the epoch);
-//   consumer: wave 0 polls the producers' flags (relaxed agent loads, one lane per flag,
-//     `s_sleep` between polls), a workgroup barrier, then EVERY load of handed-off bytes is
-//     an `sc1` load (bypasses the CU's L1), so no acquire fence is needed;
-//   no buffer is written twice in a launch (every block writes its own state buffer; the
-//   adjoint's indicator partials have one row per block), so no cache line another
-//   workgroup reads can change after it was read.
-// Epochs: a 64-bit take counter that only grows numbers the launches (value / items) and the
-// items (value % items); the flags hold the launch's epoch, so no memset precedes a launch
-// of the same shape and HIP-graph replays work.  Every poll is bounded: a producer that never
-// finishes (a bug) sets the error word after ~2^20 polls and every waiter gives up, so the
-// launch always ends.  A work item that gave up writes NaN over what it publishes, so the
-// indicator and the fused refine value turn non-finite; the error is also raised in mapped
-// host memory, which makes the plan's next sweep call fail, and dg_sweep_status() reports
-// and clears it.
-// The results are bit-identical to the launch-per-block pair with the same steps per block
-// (same tile arithmetic; the indicator's block partials are added in launch order).
-#include "dg_rec_tiles.h"
+// dg_sweep.hip — the dataflow sweep (dg_sweep_kernel.h) at Np = 2..5, per-level exchange; the host
+// helpers and the dispatch over the three translation units.
+#include "dg_sweep_kernel.h"
 
 namespace {
-using namespace dgk;
-using namespace dgr;
-
-constexpr int kSweepMaxSteps = 40;   // steps per sweep (the forward blocks' constants are kernargs)
-constexpr int kSweepMaxBlocks = 8;   // blocks per direction (kSweepMaxSteps / 5)
-// control words (uint32 index): a 64-bit take counter, the error word, a 64-bit arrival
-// counter of the fused refine decision, then one flag per item
-constexpr int kSyncHead = 0, kSyncErr = 2, kSyncArrive = 4, kSyncFlags = 16;
-constexpr int kSweepSpinLimit = 1 << 20;
-
-template <int NP, int MSF> struct SweepArgs {
-  RpOp<NP> c;
-  double bnd[(kSweepMaxSteps / MSF) * (MSF * 6 + 1)];  // block b's rp_block_bnd at b*(6 MSF+1)
-  double* U[kSweepMaxBlocks + 1];  // forward block b reads U[b] (U[0] = u0), writes U[b+1]
-  double* W[kSweepMaxBlocks + 1];  // adjoint block a reads W[a] (terminal weight), writes W[a+1]
-  double* rec;
-  double* eta;
-  double* part;                    // (nbA - 1) rows of ktot: the adjoint blocks' partial eta
-  const double* scale;
-  uint32_t* sync;                  // kSync* words, then one flag per item
-  uint64_t* trace;                 // nullable: per item {dequeued, producers done, published,
-                                   // XCC id << 32 | workgroup id} (wall clock, 100 MHz)
-  int64_t* am_idx;                 // nullable: the fused refine decision, dg_argmax_ex(|eta|)
-  double* am_val;
-  int64_t* am_nf;
-  double* am_pv;                   // per last-block tile: its (|eta|, element) winner
-  int64_t* am_pi;
-  uint32_t* err_host;              // nullable: mapped host word, raised with the error word
-  int32_t nbF, nbA, nTF, nTA;
-  int32_t nsteps;
-  int32_t mode;                    // kEta* bits (0: no indicator)
-  int32_t spin_limit;
-  int32_t take;                    // 0: items from the take counter; 1: item = workgroup id
-};
-
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Wave 0: wait until flags[0..nd) all hold `epoch` (one lane per flag, nd <= 64).  Returns
-// true (wave-uniform) if it gave up: after `limit` polls (a producer that never finishes; the
-// sweep's error word and the host-visible flag are raised) or on seeing the error word.
-__device__ __forceinline__ bool sweep_wait(const uint32_t* flags, int nd, uint32_t epoch,
-                                           uint32_t* sync, uint32_t* err_host, int limit) {
-  const int l = threadIdx.x & 63;
-  bool ok = l >= nd;
-  if (!ok) ok = ld_agent(flags + l) == epoch;
-  int spins = 0;
-  while (!__all(ok)) {
-    __builtin_amdgcn_s_sleep(2);
-    if (!ok) ok = ld_agent(flags + l) == epoch;
-    if (++spins >= limit) {
-      if (l == 0) {
-        st_agent(sync + kSyncErr, 1u);
-        if (err_host)
-          __hip_atomic_store(err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      return true;
-    }
-    if ((spins & 255) == 0 && ld_agent(sync + kSyncErr) != 0u) return true;  // someone gave up
-  }
-  return false;
-}
-
-// A work item that gave up computed on inputs that may not have been ready: it overwrites
-// what it publishes with NaN (write-through, like the outputs), so every consumer, the
-// indicator and the fused refine decision turn non-finite and the callers' checks fire.
-template <int LB>
-__device__ __forceinline__ void poison_run(double* __restrict__ g, int64_t o0, int64_t count) {
-  if (count <= 0) return;
-  const __amdgpu_buffer_rsrc_t r = wt_rsrc(g + o0);
-  const double q = __builtin_nan("");
-  for (int64_t v = threadIdx.x; v < count; v += LB) wt_st8(r, uint32_t(v) * 8u, q);
-}
-
-// Winner of (v, i) over the NW-wave workgroup under am_better; valid in thread 0.  sv / si:
-// NW LDS slots of the caller's own (not aliased with a tile image another wave may read).
-template <int NW>
-__device__ __forceinline__ void wg_argmax(double& v, int64_t& i, double* sv, int64_t* si) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double ov = __shfl_xor(v, off);
-    const int64_t oi = __shfl_xor(i, off);
-    if (am_better(ov, oi, v, i)) {
-      v = ov;
-      i = oi;
-    }
-  }
-  const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    sv[wv] = v;
-    si[wv] = i;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0)
-    for (int k = 1; k < NW; ++k)
-      if (am_better(sv[k], si[k], v, i)) {
-        v = sv[k];
-        i = si[k];
-      }
-}
-
-__device__ __forceinline__ void st8_agent(void* p, uint64_t bits) {
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), bits, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld8_agent(const void* p) {
-  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Occupancy target.  Both bodies live in one kernel, so its registers are the adjoint's
-// (82-92 VGPRs at Np = 4, 5 unconstrained: 2 eight-wave workgroups per CU).  Capped at 80
-// (6 waves per SIMD: 3 workgroups per CU, 3 x 41 KB of LDS) the allocator keeps every level
-// loop of the uniform-mesh kernels spill-free at Np <= 5; the few spills it adds sit outside
-// the loops (the edge tiles' prologue, the indicator's partial-row combine).  Np = 6 spills
-// inside a loop at 80, and the non-uniform bodies (the metric per element) spill more: they
-// keep the unconstrained count.  (Np 2, 3 fit 6 waves unconstrained.)
-// At Np = 2 the bodies fit 8 waves per SIMD by VGPRs (57) but not by SGPRs: 99 SGPRs admit 6
-// (MI355X_MICROARCH.md, residency: floor(800 / (ceil(sgpr/16)*16 + 16))).  Asked for 8, the
-// compiler keeps 78 SGPRs and 58 VGPRs without spilling, and 4- or 8-wave workgroups then fill
-// 32 wave slots per CU: N = 1 +4-6 % (6.09 / 6.17e11 against 5.88 / 5.79e11 for the 12-wave
-// default, profiles/r04/wpe8/).  Np = 3 spills 28 B per lane at 8 and gains nothing.
-template <int NP, bool UNI, int NW = 8> struct SweepOcc {
-  static constexpr int waves_per_simd =
-      (UNI && NP == 2 && (NW == 4 || NW == 8)) ? 8 : (UNI && NP <= 5) ? 6 : 1;  // 1: none
-};
-
-template <int NP, bool UNI, int NW, int MSF, int MSA, int E>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
-    E == 2 ? SweepOcc<NP, UNI, NW>::waves_per_simd : 1))) void k_sweep_rp(SweepArgs<NP, MSF> a) {
-  using G = RpGeo<NP, NW, E>;
-  constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
-  constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;
-  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MSF * 6 + 1];
-  __shared__ uint32_t s_item, s_epoch, s_last, s_bad;
-  __shared__ double s_av[NW];
-  __shared__ int64_t s_ai[NW];
-  uint32_t* sync = a.sync;
-  uint32_t* flags = sync + kSyncFlags;
-  const int tid = threadIdx.x;
-  const int64_t ktot = a.c.ktot;
-  const int nTF = a.nTF, nTA = a.nTA, nbF = a.nbF, nbA = a.nbA;
-  const int64_t nF = int64_t(nbF) * nTF;
-  const int64_t nItems = nF + int64_t(nbA) * nTA;
-  if (tid == 0) {
-    if (a.take) {
-      // item = workgroup id: each XCD starts its workgroups in id order, so the smallest
-      // unfinished item is always running or next to start on its XCD (no deadlock at any
-      // residency).  Every launch publishes every item's flag, so the item's own flag holds
-      // the previous launch's epoch: no shared counter (one contended atomic per workgroup).
-      s_item = blockIdx.x;
-      s_epoch = ld_agent(flags + blockIdx.x) + 1u;
-    } else {
-      // The take counter only grows: every launch of this shape takes exactly nItems values
-      // (one per workgroup), so h / nItems numbers the launch (its epoch - 1) and h % nItems
-      // is the item -- no reset, no generation word, no exit counter.  (The host zeroes the
-      // control words when a launch of another shape reuses them.)
-      const uint64_t h = __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(sync + kSyncHead),
-                                                uint64_t(1), __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      s_epoch = uint32_t(h / uint64_t(nItems)) + 1u;
-      s_item = uint32_t(h % uint64_t(nItems));
-    }
-    s_bad = 0u;
-  }
-  __syncthreads();
-  const int64_t item = s_item;
-  const uint32_t epoch = s_epoch;
-  const uint64_t t_deq = a.trace ? uint64_t(wall_clock64()) : 0;
-  {
-    // decode the item and the range of flags it waits for
-    const bool fwd = item < nF;
-    int blk, j;
-    int64_t d0 = 0;
-    int nd = 0;
-    if (fwd) {
-      blk = int(item / nTF);
-      j = int(item - int64_t(blk) * nTF);
-      if (blk > 0) {  // the previous block's tiles j-1..j+1 (halo < TEF)
-        const int lo = j > 0 ? j - 1 : 0, hi = j + 1 < nTF ? j + 1 : nTF - 1;
-        d0 = int64_t(blk - 1) * nTF + lo;
-        nd = hi - lo + 1;
-      }
-    } else {
-      const int64_t i2 = item - nF;
-      blk = int(i2 / nTA);
-      j = int(i2 - int64_t(blk) * nTA);
-      if (blk == 0) {  // the last forward block's tiles covering the input + record range
-        int64_t elo = int64_t(j) * TEA - HA, ehi = int64_t(j + 1) * TEA + HA;
-        elo = elo > 0 ? elo : 0;
-        ehi = ehi < ktot - 1 ? ehi : ktot - 1;
-        const int lo = int(elo / TEF), hi = int(ehi / TEF);
-        d0 = int64_t(nbF - 1) * nTF + lo;
-        nd = hi - lo + 1;
-      } else {
-        const int lo = j > 0 ? j - 1 : 0, hi = j + 1 < nTA ? j + 1 : nTA - 1;
-        d0 = nF + int64_t(blk - 1) * nTA + lo;
-        nd = hi - lo + 1;
-      }
-    }
-    if (tid < 64 && nd > 0) {
-      const bool gave_up = sweep_wait(flags + d0, nd, epoch, sync, a.err_host, a.spin_limit);
-      if (tid == 0 && gave_up) s_bad = 1u;
-    }
-    // no acquire fence: every load of handed-off bytes below is an sc1 load; this only keeps
-    // the compiler from hoisting them above the poll
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __syncthreads();
-    const uint64_t t_ready = a.trace ? uint64_t(wall_clock64()) : 0;
-    using SA = SweepArgs<NP, MSF>;
-    const DG_KAS char* ka = kernarg_tail_k<decltype(&k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), SA>();
-    const OpSrc<NP> os = op_src<NP>(a.c, ka + offsetof(SA, c));
-    if (fwd) {
-      const int64_t e0 = int64_t(j) * TEF - HF;
-      const double* kb = reinterpret_cast<const double*>(
-                             kernarg_tail<decltype(&k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), SA>() +
-                             offsetof(SA, bnd)) + blk * (MSF * 6 + 1);
-      const int64_t n0 = int64_t(blk) * MSF;
-      const bool jend = blk == a.nbF - 1;
-      if (edge_tile(e0, G::T, ktot, a.c.K))
-        rp_step_tile<NP, UNI, NW, E, MSF, true, true>(lds, j, a.U[blk], a.rec, a.U[blk + 1],
-                                                      a.scale, a.c, os, kb, n0, jend);
-      else
-        rp_step_tile<NP, UNI, NW, E, MSF, false, true>(lds, j, a.U[blk], a.rec, a.U[blk + 1],
-                                                       a.scale, a.c, os, kb, n0, jend);
-      if (s_bad) {  // after the body's final barrier: its stores are issued, ours follow
-        const int64_t o0 = int64_t(j) * TEF * NP, nd = ktot * NP;
-        poison_run<64 * NW>(a.U[blk + 1], o0, (nd - o0) < int64_t(TEF) * NP ? nd - o0
-                                                                            : int64_t(TEF) * NP);
-      }
-    } else {
-      const int64_t e0 = int64_t(j) * TEA - HA;
-      const bool lastb = blk == a.nbA - 1;
-      EtaSink es;
-      es.eta = a.eta;
-      es.part_out = (a.mode && !lastb) ? a.part + int64_t(blk) * ktot : nullptr;
-      es.part_in = a.part;
-      es.part_ld = ktot;
-      es.nparts = lastb ? a.nbA - 1 : 0;
-      es.mode = a.mode;
-      es.argmax = lastb && a.am_idx != nullptr;
-      es.bv = -INFINITY;  // the weakest candidate (dg_argmax's convention)
-      es.bi = INT64_MAX;
-      const int64_t n0 = int64_t(a.nsteps) - int64_t(blk + 1) * MSA;
-      if (edge_tile(e0, G::T, ktot, a.c.K))
-        rp_adj_tile<NP, UNI, NW, E, MSA, true, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
-                                                     a.scale, a.c, os, n0);
-      else
-        rp_adj_tile<NP, UNI, NW, E, MSA, false, true>(lds, j, a.W[blk], a.W[blk + 1], a.rec, es,
-                                                      a.scale, a.c, os, n0);
-      if (s_bad) {
-        const int64_t o0 = int64_t(j) * TEA, nd = ktot * NP;
-        const int64_t ne = (ktot - o0) < TEA ? ktot - o0 : int64_t(TEA);
-        poison_run<64 * NW>(a.W[blk + 1], o0 * NP, (nd - o0 * NP) < int64_t(TEA) * NP
-                                                       ? nd - o0 * NP : int64_t(TEA) * NP);
-        if (a.mode) poison_run<64 * NW>(es.part_out ? es.part_out : a.eta, o0, ne);
-        es.bv = __builtin_nan("");
-      }
-      if (es.argmax) {  // the tile's winner, a hand-off to the last arriving tile
-        wg_argmax<NW>(es.bv, es.bi, s_av, s_ai);
-        if (tid == 0) {
-          st8_agent(a.am_pv + j, __builtin_bit_cast(uint64_t, es.bv));
-          st8_agent(a.am_pi + j, uint64_t(es.bi));
-        }
-      }
-    }
-    // publish: every wave's write-through stores have completed, then one flag store
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) st_agent(flags + item, epoch);
-    if (!fwd && blk == nbA - 1 && a.am_idx != nullptr) {
-      // Fused refine decision: the last block's tiles arrive on a counter that grows by nTA
-      // per launch; the one whose add completes a launch's count reduces the nTA winners
-      // (published above, write-through, drained before the add) with sc1 loads.
-      if (tid == 0) {
-        const uint64_t old = __hip_atomic_fetch_add(
-            reinterpret_cast<uint64_t*>(sync + kSyncArrive), uint64_t(1), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        s_last = ((old + 1) % uint64_t(nTA)) == 0 ? 1u : 0u;
-      }
-      __syncthreads();
-      if (s_last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double v = -INFINITY;
-        int64_t i = INT64_MAX;
-        for (int q = tid; q < nTA; q += 64 * NW) {
-          const double pv = __builtin_bit_cast(double, ld8_agent(a.am_pv + q));
-          const int64_t pi = int64_t(ld8_agent(a.am_pi + q));
-          if (am_better(pv, pi, v, i)) {
-            v = pv;
-            i = pi;
-          }
-        }
-        wg_argmax<NW>(v, i, s_av, s_ai);
-        if (tid == 0) {
-          if (ld_agent(sync + kSyncErr) != 0u) v = __builtin_nan("");  // a work item gave up
-          a.am_idx[0] = i;
-          if (a.am_val) a.am_val[0] = v;
-          if (a.am_nf && !isfinite(v)) a.am_nf[0] += 1;
-        }
-      }
-    }
-    if (a.trace && tid == 0) {
-      uint32_t xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      uint64_t* tr = a.trace + 4 * item;
-      tr[0] = t_deq;
-      tr[1] = t_ready;
-      tr[2] = uint64_t(wall_clock64());
-      tr[3] = (uint64_t(xcc) << 32) | blockIdx.x;
-    }
-  }
-}
-
-static_assert(kSweepMaxBlocks + 1 == sizeof(SweepBufs::U) / sizeof(double*), "SweepBufs");
-
-template <int NP, bool UNI, int NW, int MSF, int MSA, int E>
-int sweep_launch(dg_plan* p, const dgk::SweepBufs& b, double t0, double dt, int nsteps,
-                 int mode, hipStream_t st) {
-  SweepArgs<NP, MSF> a;
-  if (const int rc = rp_make_op<NP>(p, dt, &a.c)) return rc;
-  const int nbF = nsteps / MSF, nbA = nsteps / MSA;
-  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt (One_code.mlx:139)
-  tn[0] = t0;
-  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
-  for (int bk = 0; bk < nbF; ++bk)
-    rp_block_bnd(p, MSF, &tn[size_t(bk) * MSF], dt, a.bnd + bk * (MSF * 6 + 1));
-  for (int i = 0; i <= kSweepMaxBlocks; ++i) {
-    a.U[i] = b.U[i];
-    a.W[i] = b.W[i];
-  }
-  a.rec = b.rec;
-  a.eta = b.eta;
-  a.part = b.part;
-  a.scale = p->d_scale;
-  a.sync = b.sync;
-  a.trace = p->sweep_trace;
-  a.am_idx = b.am_idx;
-  a.am_val = b.am_val;
-  a.am_nf = b.am_nf;
-  a.am_pv = b.am_pv;
-  a.am_pi = b.am_pi;
-  a.nbF = nbF;
-  a.nbA = nbA;
-  using G = RpGeo<NP, NW, E>;
-  a.nTF = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSF>::F));
-  a.nTA = int(grid_for(p->ktot, G::T - 2 * RpHalo<MSA>::A));
-  a.nsteps = nsteps;
-  a.mode = mode;
-  a.err_host = b.err_host;
-  a.spin_limit = b.spin_limit > 0 ? b.spin_limit : kSweepSpinLimit;
-  a.take = b.take;
-  const int64_t items = int64_t(nbF) * a.nTF + int64_t(nbA) * a.nTA;
-  hipLaunchKernelGGL((k_sweep_rp<NP, UNI, NW, MSF, MSA, E>), dim3(unsigned(items)), dim3(64 * NW), 0,
-                     st, a);
-  HIP_TRY(hipGetLastError());
-  return DG_OK;
-}
-
-template <int NP, bool UNI, int NW, int E>
-int sweep_shape_launch(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0,
-                       double dt, int nsteps, int mode, hipStream_t st) {
-  if constexpr (NW > 8) {  // the wide tiles: 20- or 10-step forward, 10-step adjoint blocks
-    if (msa == 10 && msf == 20) return sweep_launch<NP, UNI, NW, 20, 10, E>(p, b, t0, dt, nsteps, mode, st);
-    if (msa == 10 && msf == 10) return sweep_launch<NP, UNI, NW, 10, 10, E>(p, b, t0, dt, nsteps, mode, st);
-    return fail(DG_ERR_ARG, "dataflow sweep: 12 or 16 waves take 10- or 20-step forward and "
-                            "10-step adjoint blocks");
-  }
-  if (msa == 10) {
-    if constexpr (NW * E >= 16)  // 20-step forward blocks need 1024-element tiles
-      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 10, E>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 10, E>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 10, E>(p, b, t0, dt, nsteps, mode, st);
-  } else if (msa == 5) {
-    if constexpr (NW * E >= 16)  // 20-step forward blocks need 1024-element tiles
-      if (msf == 20) return sweep_launch<NP, UNI, NW, 20, 5, E>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 10) return sweep_launch<NP, UNI, NW, 10, 5, E>(p, b, t0, dt, nsteps, mode, st);
-    if (msf == 5) return sweep_launch<NP, UNI, NW, 5, 5, E>(p, b, t0, dt, nsteps, mode, st);
-  }
-  return fail(DG_ERR_ARG, "dataflow sweep: unsupported steps per block for this tile width");
-}
-
-template <int NP, int NW, int E = 2>
-int sweep_uni(dg_plan* p, int msf, int msa, const dgk::SweepBufs& b, double t0, double dt,
-              int nsteps, int mode, hipStream_t st) {
-  return p->uniform
-             ? sweep_shape_launch<NP, true, NW, E>(p, msf, msa, b, t0, dt, nsteps, mode, st)
-             : sweep_shape_launch<NP, false, NW, E>(p, msf, msa, b, t0, dt, nsteps, mode, st);
-}
-
 // Tiles of 128 * waves elements on workgroups of `waves` waves: 8 (1024 elements, the
 // default) or 4 (512: tile width 1).  Workgroups of 5, 6 and 10 waves (which fill the 20 wave
 // slots per CU the 88-VGPR bodies leave, where 8-wave groups use 16) measured 17-27 % slower
 // at N = 4, K = 2^20 (profiles/r03/waves2/: more items and their per-item latency, or a
-// barrier over 10 waves) and were dropped.
+// barrier over 10 waves) and were dropped.  With the overlapped waves (p->sweep_exchange = 1,
+// dg_ovl_tiles.h) tiles of waves * 116 + 12 elements on 8, 12 or 16 waves.
 template <int NP>
-int sweep_np(dg_plan* p, int waves, int msf, int msa, const dgk::SweepBufs& b, double t0,
+int sweep_np_x0(dg_plan* p, int waves, int msf, int msa, const dgk::SweepBufs& b, double t0,
              double dt, int nsteps, int mode, hipStream_t st) {
   if constexpr (NP <= 3) {  // four elements per lane (DG_TUNE_SWEEP_LANE_ELEMENTS)
     if (p->sweep_lane_elems == 4) {
@@ -462,22 +31,83 @@ int sweep_np(dg_plan* p, int waves, int msf, int msa, const dgk::SweepBufs& b, d
 
 namespace dgk {
 
-int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps) {
-  const int T = 64 * p->sweep_lane_elems * waves;
-  const int64_t nTF = grid_for(p->ktot, T - 2 * ((msf * 5 + 2) & ~1));
-  const int64_t nTA = grid_for(p->ktot, T - 2 * ((msa * 5 + 1) & ~1));
+int sweep_launch_lo(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b,
+                    double t0, double dt, int nsteps, int mode, hipStream_t st) {
+  int rc = DG_OK;
+  switch (p->NP) {
+    case 2: rc = sweep_np_x0<2>(p, waves, msf, msa, b, t0, dt, nsteps, mode, st); break;
+    case 3: rc = sweep_np_x0<3>(p, waves, msf, msa, b, t0, dt, nsteps, mode, st); break;
+    case 4: rc = sweep_np_x0<4>(p, waves, msf, msa, b, t0, dt, nsteps, mode, st); break;
+    case 5: rc = sweep_np_x0<5>(p, waves, msf, msa, b, t0, dt, nsteps, mode, st); break;
+    default: return fail(DG_ERR_ARG, "unsupported Np");
+  }
+  return rc;
+}
+
+
+int sweep_launch_lo(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,
+                    double dt, int nsteps, int mode, hipStream_t st);
+int sweep_launch_hi(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,
+                    double dt, int nsteps, int mode, hipStream_t st);
+int sweep_launch_ov(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,
+                    double dt, int nsteps, int mode, hipStream_t st);
+
+
+int sweep_tile_elems(const dg_plan* p, int waves) {
+  return p->sweep_exchange == 1 ? waves * kOvS + 2 * kOvG : 64 * p->sweep_lane_elems * waves;
+}
+
+int sweep_waves_per_simd(const dg_plan* p, int waves) {
+  const int E = p->sweep_lane_elems, X = p->sweep_exchange;
+  if (E != 2) return 0;
+  int w = 0;
+  // SweepOcc<NP, UNI, NW, X>::waves_per_simd, evaluated on the host (1 there means none)
+  auto occ = [&](auto np_tag) {
+    constexpr int NP = decltype(np_tag)::value;
+    auto pick = [&](auto uni_tag) {
+      constexpr bool UNI = decltype(uni_tag)::value;
+      switch (waves) {
+        case 4: return X ? 0 : SweepOcc<NP, UNI, 4, 0>::waves_per_simd;
+        case 8: return X ? SweepOcc<NP, UNI, 8, 1>::waves_per_simd : SweepOcc<NP, UNI, 8, 0>::waves_per_simd;
+        case 12: return X ? SweepOcc<NP, UNI, 12, 1>::waves_per_simd : SweepOcc<NP, UNI, 12, 0>::waves_per_simd;
+        case 16: return X ? SweepOcc<NP, UNI, 16, 1>::waves_per_simd : SweepOcc<NP, UNI, 16, 0>::waves_per_simd;
+        default: return 0;
+      }
+    };
+    w = p->uniform ? pick(std::true_type{}) : pick(std::false_type{});
+  };
+  switch (p->NP) {
+    case 2: occ(std::integral_constant<int, 2>{}); break;
+    case 3: occ(std::integral_constant<int, 3>{}); break;
+    case 4: occ(std::integral_constant<int, 4>{}); break;
+    case 5: occ(std::integral_constant<int, 5>{}); break;
+    case 6: occ(std::integral_constant<int, 6>{}); break;
+    case 7: occ(std::integral_constant<int, 7>{}); break;
+    case 8: occ(std::integral_constant<int, 8>{}); break;
+    case 9: occ(std::integral_constant<int, 9>{}); break;
+    default: break;
+  }
+  return w == 1 ? 0 : w;
+}
+
+int64_t sweep_items(const dg_plan* p, int waves, int msf, int msa, int nsteps, int64_t elems) {
+  const int64_t n = elems >= 0 ? elems : p->ktot;
+  const int T = sweep_tile_elems(p, waves);
+  const int64_t nTF = grid_for(n, T - 2 * ((msf * 5 + 2) & ~1));
+  const int64_t nTA = grid_for(n, T - 2 * ((msa * 5 + 1) & ~1));
   return int64_t(nsteps / msf) * nTF + int64_t(nsteps / msa) * nTA;
 }
 
-int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa) {
-  return grid_for(p->ktot, 64 * p->sweep_lane_elems * waves - 2 * ((msa * 5 + 1) & ~1));
+int64_t sweep_tiles_adj(const dg_plan* p, int waves, int msa, int64_t elems) {
+  const int64_t n = elems >= 0 ? elems : p->ktot;
+  return grid_for(n, sweep_tile_elems(p, waves) - 2 * ((msa * 5 + 1) & ~1));
 }
 
 int sweep_launch_rec(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b, double t0,
                      double dt, int nsteps, int mode, hipStream_t st) {
-  int rc = DG_OK;
-  DG_DISPATCH_NP(p->NP, rc = sweep_np<NP>(p, waves, msf, msa, b, t0, dt, nsteps, mode, st));
-  return rc;
+  if (p->sweep_exchange == 1) return sweep_launch_ov(p, waves, msf, msa, b, t0, dt, nsteps, mode, st);
+  if (p->NP <= 5) return sweep_launch_lo(p, waves, msf, msa, b, t0, dt, nsteps, mode, st);
+  return sweep_launch_hi(p, waves, msf, msa, b, t0, dt, nsteps, mode, st);
 }
 
 int sweep_sync_words() { return kSyncFlags; }

@@ -137,7 +137,7 @@ class DGAdvection1D:
   def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None,
            rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
            rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None, rec_sweep=None,
-           sweep_waves=None, sweep_lane_elements=None, sweep_take=None):
+           sweep_waves=None, sweep_lane_elements=None, sweep_take=None, sweep_exchange=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -156,7 +156,9 @@ class DGAdvection1D:
     workgroup waves, tiles of 128 * waves elements in both directions (0: as the record tile
     width; bit-identical at any value); ``sweep_lane_elements`` (2, or 4 at N <= 2): consecutive
     elements per lane of its tiles; ``sweep_take`` (0 / 1): its work items from one take
-    counter or by workgroup id (bit-identical)."""
+    counter or by workgroup id (bit-identical); ``sweep_exchange`` (0 / 1): its tiles exchange
+    faces through LDS with a barrier per Horner level, or on overlapped waves by DPP with one
+    LDS exchange and barrier per step (tiles of waves * 116 + 12 elements; bit-identical)."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
                      (_lib.DG_TUNE_REC_SWEEP, rec_sweep),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
@@ -165,7 +167,8 @@ class DGAdvection1D:
                      (_lib.DG_TUNE_REC_FWD_TILE_WIDTH, rec_fwd_tile_width),
                      (_lib.DG_TUNE_SWEEP_WAVES, sweep_waves),
                      (_lib.DG_TUNE_SWEEP_LANE_ELEMENTS, sweep_lane_elements),
-                     (_lib.DG_TUNE_SWEEP_TAKE, sweep_take)):
+                     (_lib.DG_TUNE_SWEEP_TAKE, sweep_take),
+                     (_lib.DG_TUNE_SWEEP_EXCHANGE, sweep_exchange)):
       if val is not None:
         _lib.check(self._lib.dg_plan_tune(self._plan, key, int(val)), "dg_plan_tune")
     if xcd_order is not None:
@@ -375,6 +378,23 @@ class DGAdvection1D:
                "dg_plan_query_sweep_ex")
     out = (bool(q[0]), int(q[1]), int(q[2]), int(q[3]))
     return out + (int(q[4]), int(q[5])) if tile else out
+
+  def query_sweep_kernel(self, nsteps):
+    """The dataflow launch's kernel for an ``nsteps`` sweep, as a profile must match it:
+    dict(Np, uniform, waves, msf, msa, lane_elements, exchange, waves_per_simd, name) with
+    name the rocprof kernel name prefix ``k_sweep_rp<Np, uniform, waves, msf, msa, E, X>``;
+    None when ``sweep_rec`` runs the two launch chains."""
+    q = (ctypes.c_int64 * 8)()
+    _lib.check(self._lib.dg_plan_query_sweep_kernel(self._plan, int(nsteps), q),
+               "dg_plan_query_sweep_kernel")
+    if q[0] == 0:
+      return None
+    keys = ("Np", "uniform", "waves", "msf", "msa", "lane_elements", "exchange",
+            "waves_per_simd")
+    d = {k: int(v) for k, v in zip(keys, q)}
+    d["name"] = (f"k_sweep_rp<{d['Np']}, {'true' if d['uniform'] else 'false'}, {d['waves']}, "
+                 f"{d['msf']}, {d['msa']}, {d['lane_elements']}, {d['exchange']}>")
+    return d
 
   def sweep_trace(self, trace):
     """Profiling: record per work item of every later dataflow sweep {taken, producers done,

@@ -99,12 +99,13 @@ def p_flops_per_update(Np):
 def halo_factor(T, H):
   """Lanes issued per useful lane of a tile of T elements whose launch writes T - 2 H."""
   return T / float(T - 2 * H)
-# Profiles of bench configurations (profiles/r04/collect.sh): each directory holds the per-launch
+# Profiles of bench configurations (profiles/r05/collect.sh): each directory holds the per-launch
 # PMC traffic of the sweep kernel (pmc_traffic.json) and its SQ passes (sq_summary.json: issued
-# fp64 instructions); a bench line uses the one whose N, K, shape and kernel instantiation match
+# fp64 instructions); a bench line uses the one whose N, K, shape and kernel (instantiation and
+# occupancy target, `sweep_kernel`) match, else reports traffic null
 PROFILE_DIRS = {
-    "jumps": [os.path.join(ROOT, "profiles", "r04", d)
-              for d in ("headline_w12", "N8_dflow", "N1_w8", "N1", "headline")],
+    "jumps": [os.path.join(ROOT, "profiles", "r05", d)
+              for d in ("headline", "N1", "N2", "N6", "N8", "c4")],
     "snapshots": [os.path.join(ROOT, "profiles", "r02")],
     "p": [os.path.join(ROOT, "profiles", "r04", "p")]}
 PROFILE_TRAFFIC_FILE = {"snapshots": "pmc_traffic_snapshots.json"}  # default pmc_traffic.json
@@ -235,6 +236,17 @@ def stream_copy_gbs(dev, nbytes=1 << 30, reps=10):
     ts.append(e0.elapsed_time(e1) * 1e-3)
   del src, dst
   return 2.0 * nbytes / float(np.median(ts)) / 1e9
+
+
+BASELINE_METRIC = "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6"
+
+
+def metric_name(N, K):
+  """BASELINE.json's metric string for its own configuration (N = 4, K = 2^20); the same
+  metric with the run's actual N and K otherwise (config 3, 4 and 5 lines)."""
+  if N == 4 and K == 1 << 20:
+    return BASELINE_METRIC
+  return f"DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N={N}, K={K}"
 
 
 def cpu_baseline(N, K, nsteps, threads=1, indicator="jump", ics=1, ics_total=1):
@@ -471,7 +483,7 @@ def main_config3(args, world, rank, dev):
   fwd_bytes = (8.0 + 8.0 * ms) * Np * k_mid
   adj_bytes = 24.0 * Np * k_mid + 16.0 * k_mid
   out = {
-      "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
+      "metric": metric_name(N, K),
       "value": total / elapsed,
       "unit": "DOF-updates/s",
       "n_gpus": world,
@@ -827,11 +839,14 @@ def main(argv=None):
   fwd_gbs = fwd_bytes / (fwd_launch_us * 1e-6) / 1e9
   traffic = traffic_src = None
   prof_key = "p" if pmode else args.record
-  # a dataflow profile counts only for the same kernel instantiation (Np, mesh, waves, blocks)
-  kinst = (f"k_sweep_rp<{Np}, true, {sweep_waves}, {fchunks[0]}, {chunks[0]}"
-           if pairs and dataflow else None)
-  same_kernel = lambda names: kinst is None or any(  # noqa: E731
-      str(n).startswith(kinst) for n in (names or []))
+  # a dataflow profile counts only for the same kernel: its template instantiation (Np, mesh,
+  # waves, blocks, lane elements, face exchange) and its occupancy target, which is an
+  # attribute outside the name (round 4's Np = 2 line read a profile of the 6-waves-per-SIMD
+  # build of the same name); a profile without that record matches nothing
+  ksig = sweep.op.query_sweep_kernel(nsteps) if pairs and dataflow else None
+  same_kernel = lambda tr: ksig is None or (  # noqa: E731
+      tr.get("sweep_kernel") == ksig
+      and any(str(n).startswith(ksig["name"]) for n in (tr.get("adj_kernel") or [])))
   prof_dir = None  # the matching profile directory (its SQ summary is read below)
   for d in PROFILE_DIRS[prof_key]:
     try:
@@ -843,7 +858,7 @@ def main(argv=None):
         and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
         and tr.get("record", "snapshots") == args.record
         and tr.get("indicator", "jump") == args.indicator
-        and same_kernel(tr.get("adj_kernel"))):
+        and same_kernel(tr)):
       traffic = tr.get("adj_bytes_per_launch")
       traffic_src = os.path.relpath(d, ROOT)
       prof_dir = d
@@ -892,7 +907,7 @@ def main(argv=None):
     halo_adj = (f_fl * halo_fwd + a_fl * halo_adj) / (f_fl + a_fl)
   decision = refine_margin(sweep, one_step) if world == 1 and not args.no_margin else None
   out = {
-      "metric": "DOF-updates/sec, 1D DG advection fwd+adjoint sweep, N=4, K=1e6",
+      "metric": metric_name(N, K),
       "value": value,
       "unit": "DOF-updates/s",
       "n_gpus": world,
@@ -1026,6 +1041,7 @@ def main(argv=None):
                        "refine_to_host": "written by the launch into pinned memory (dg_host_alias)"
                                          if res_alias is not None else "async copy",
                        "work_items": sweep.op.query_sweep(nsteps)[3],
+                       "kernel": ksig,
                        "status": sweep.op.sweep_status()}
     if out["dataflow"]["status"]:
       raise RuntimeError("a dataflow work item gave up waiting for a producer")

@@ -129,22 +129,29 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             2 (default), or 4 at Np <= 3 on 4- or 8-wave workgroups (tiles
  *                             of 256 * waves elements: half the barriers per element, half the
  *                             halo share).  Bit-identical results
- *   DG_TUNE_SWEEP_TAKE        how a dataflow work item is assigned: 0 (default) the next value
- *                             of one take counter, 1 the workgroup id (no shared atomic; the
- *                             launch epoch read from the item's own flag).  Bit-identical
+ *   DG_TUNE_SWEEP_TAKE        0 only: dataflow work items come from one take counter (round 4's
+ *                             1, item = workgroup id, relied on in-order dispatch per XCD and
+ *                             was removed in round 5; 1 is an argument error)
+ *   DG_TUNE_SWEEP_EXCHANGE    how the dataflow sweep's tiles exchange element faces: 0 (default)
+ *                             through LDS with a workgroup barrier per Horner level; 1
+ *                             overlapped waves: faces within a wave by DPP, one LDS exchange of
+ *                             6 ghost elements per wave end and one barrier per time step
+ *                             (tiles of waves * 116 + 12 elements on 8, 12 or 16 (Np <= 5)
+ *                             waves; 20- or 10-step forward and 10-step adjoint blocks).
+ *                             Bit-identical results
  *   DG_TUNE_SWEEP_SPIN_LIMIT  diagnostics/tests: polls a dataflow work item makes before it
  *                             gives up waiting for a producer (0: the default, ~2^20; 1 makes
  *                             the watchdog fire on any multi-block sweep)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
  * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
- * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_TAKE. */
+ * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
        DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10,
        DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12,
        DG_TUNE_SWEEP_SPIN_LIMIT = 13, DG_TUNE_SWEEP_WAVES = 14,
-       DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16 };
+       DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16, DG_TUNE_SWEEP_EXCHANGE = 17 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
@@ -176,7 +183,10 @@ int dg_plan_set_physics(dg_plan* plan, int flux, int limiter);
 
 /* Grow the plan's device mesh and scratch buffers to hold K_capacity elements per trajectory,
  * so that dg_plan_refine can add elements without reallocating.  Synchronous (waits for the
- * device); never shrinks; a no-op when the capacity suffices. */
+ * device); never shrinks; a no-op when the capacity suffices.  The dataflow sweep's scratch is
+ * sized for the reserved capacity, so refines within it reuse it; a growing reserve frees the
+ * plan's old scratch (also scratch regions earlier sweeps outgrew), so HIP graphs captured
+ * before it must be re-captured. */
 int dg_plan_reserve(dg_plan* plan, int64_t K_capacity);
 
 /* Refine on the device: split element idx[0] (device int64 in [0, K), e.g. dg_argmax's
@@ -298,6 +308,12 @@ int dg_lserk4_sweep_refine(dg_plan* plan, const double* u0, double* uN, double* 
 int dg_plan_query_sweep(const dg_plan* plan, int nsteps, int64_t out[4]);
 /* dg_plan_query_sweep plus out[4] = workgroup waves, out[5] = elements per tile. */
 int dg_plan_query_sweep_ex(const dg_plan* plan, int nsteps, int64_t out[6]);
+/* The dataflow launch's kernel for nsteps (profiling: what a PMC profile must match):
+ * out[0] = Np, out[1] = 1 on a uniform mesh, out[2] = workgroup waves, out[3] / out[4] =
+ * forward / adjoint steps per block, out[5] = elements per lane, out[6] = face exchange
+ * (DG_TUNE_SWEEP_EXCHANGE), out[7] = the occupancy target in waves per SIMD (0: none).
+ * out[0] = 0 when nsteps runs as the two launch chains. */
+int dg_plan_query_sweep_kernel(const dg_plan* plan, int nsteps, int64_t out[8]);
 /* Synchronises `stream`; *status = 0, or 1 if a dataflow sweep since the last call gave up
  * waiting for a producer (a bug, or DG_TUNE_SWEEP_SPIN_LIMIT), and clears the flag.  A work
  * item that gives up still computes, so the launch ends, but it writes NaN over its outputs

@@ -463,3 +463,87 @@ def test_four_elements_per_lane_equal_launch_chains(pkg, gpu, N, K, batch, waves
     torch.cuda.synchronize()
     e = np.abs(host(eta))
     assert int(host(res)[0]) == int(np.argmax(e)) and op.sweep_status() == 0
+
+
+@pytest.mark.parametrize("N,K,batch,waves,fsteps,nsteps,inflow,refined", [
+    (4, 9000, 1, 12, 20, 20, "a", False),    # the headline shape: 1404-element tiles
+    (4, 7000, 3, 12, 20, 40, "a2", False),   # trajectory edges inside tiles, 2 + 4 blocks
+    (4, 5000, 2, 8, 10, 20, "a", True),      # 940-element tiles, refined (non-uniform metric)
+    (1, 9000, 1, 8, 20, 20, "a", False),     # Np = 2 at 8 waves per SIMD
+    (1, 3001, 3, 16, 10, 20, "zero", False),  # 1868-element tiles, odd element count
+    (2, 6000, 1, 12, 20, 20, "a", False),
+    (3, 2000, 2, 16, 10, 30, "a", False),
+    (5, 4000, 1, 12, 20, 20, "a2", False),
+    (6, 5000, 1, 12, 10, 40, "a", False),
+    (7, 3000, 2, 8, 20, 20, "a", True),
+    (8, 6000, 1, 8, 20, 20, "a", False),     # Np = 9 (operator blocks re-read from kernargs)
+    (4, 700, 1, 12, 20, 20, "a", False),     # fewer elements than one tile's output
+])
+def test_overlapped_waves_equal_launch_chains(pkg, gpu, N, K, batch, waves, fsteps, nsteps,
+                                              inflow, refined):
+  """DG_TUNE_SWEEP_EXCHANGE = 1 (dg_ovl_tiles.h): faces within a wave by DPP, ghosts refreshed
+  through LDS once per step.  Every element's arithmetic is the pair tiles' on the same doubles,
+  so u^N, the record, w^0 and eta equal the launch chains' bit for bit; the fused refine
+  decision equals numpy's argmax of |eta|."""
+  import torch
+  v_x = np.linspace(0.0, 1.0, K + 1)
+  if refined:
+    for k in (3, 900, 901, K - 1):
+      v_x = np.insert(v_x, k + 1, 0.5 * (v_x[k] + v_x[k + 1]))
+  mesh = pkg.BaseGalerkin1D(n=N, v_x=v_x)
+  op = pkg.operators.DGAdvection1D(mesh, batch=batch, inflow=inflow)
+  op.tune(rec_steps_per_launch=10, rec_fwd_steps_per_launch=fsteps)
+  if N == 8:
+    op.tune(rec_tile_width=1, rec_fwd_tile_width=2)
+  dt = mesh.cfl_dt()
+  u0 = noisy_sine(op, 80 + N, batch)
+  ref = run_sweep(op, u0, dt, nsteps, False)
+  op.tune(sweep_waves=waves, sweep_exchange=1, rec_sweep=1)
+  on, f, a, items, w, T = op.query_sweep(nsteps, tile=True)
+  assert on and (f, a, w, T) == (fsteps, 10, waves, 116 * waves + 12)
+  for rep in range(2):
+    got = run_sweep(op, u0, dt, nsteps, True)
+    assert_same(got, ref, f"overlapped waves, N={N}, {waves} waves, rep {rep}")
+  if batch == 1:
+    rec, w_ = op.new_jumps(nsteps), op.new_field()
+    eta = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+    res = torch.zeros(3, dtype=torch.int64, device=gpu)
+    op.sweep_refine(u0, rec, w_, 0.0, dt, nsteps, eta, res[0:1], res[1:2].view(torch.float64),
+                    res[2:3])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(np.abs(host(eta)), np.abs(ref[3]))
+    e = np.abs(host(eta))
+    assert int(host(res)[0]) == int(np.argmax(e)) and op.sweep_status() == 0
+
+
+def test_refine_loop_reuses_the_sweep_scratch(pkg, gpu):
+  """An adapt loop on the public API (sweep_refine, then refine the winner, within the plan's
+  reserved capacity) must not grow device memory: the dataflow scratch is sized for the
+  capacity, so the refines reuse one region (each refine used to retire the old
+  region and allocate a slightly larger one, tens of MB per iteration at this size)."""
+  import torch
+  N, K, nsteps, iters = 4, 60000, 20, 8
+  mesh = pkg.BaseGalerkin1D(n=N, k=K)
+  op = pkg.operators.DGAdvection1D(mesh)
+  op.reserve(K + 2 * iters)
+  dt = mesh.cfl_dt()
+  field_bytes = 8 * (N + 1) * (K + iters)
+  free = []
+  for it in range(iters):
+    u0 = noisy_sine(op, 90 + it, 1)
+    rec, w = op.new_jumps(nsteps), op.new_field()
+    eta = torch.empty(op.ktot, dtype=torch.float64, device=gpu)
+    res = torch.zeros(3, dtype=torch.int64, device=gpu)
+    assert op.query_sweep(nsteps)[0]
+    op.sweep_refine(u0, rec, w, 0.0, dt, nsteps, eta, res[0:1], res[1:2].view(torch.float64),
+                    res[2:3])
+    torch.cuda.synchronize()
+    assert int(host(res)[0]) == int(np.argmax(np.abs(host(eta))))
+    op.refine(res[0:1])
+    torch.cuda.synchronize()
+    del u0, rec, w, eta
+    torch.cuda.empty_cache()
+    free.append(torch.cuda.mem_get_info(gpu)[0])
+  assert op.sweep_status() == 0
+  # after the first iteration (which allocates the scratch) free memory stays flat
+  assert free[0] - free[-1] < field_bytes, (free, field_bytes)
