@@ -29,9 +29,11 @@ DG_TUNE_SWEEP_WAVES = 14
 DG_TUNE_SWEEP_LANE_ELEMENTS = 15
 DG_TUNE_SWEEP_TAKE = 16
 DG_TUNE_SWEEP_EXCHANGE = 17
+DG_TUNE_SNAP_PAIRS = 18
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
+DG_ADJ_P_TERMINAL_PROLONG = 8
 DG_SWEEP_TERMINAL_STATE = 4
 
 _c_dbl_p = ctypes.POINTER(ctypes.c_double)

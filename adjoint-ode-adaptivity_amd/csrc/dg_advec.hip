@@ -1321,6 +1321,11 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     p->rec_tile_width = 1;
     p->rec_tile_width_fwd = 2;
   }
+  // The p-enriched estimate (dg_lserk4_adj_p, Horner form since round 5) on 256-element tiles:
+  // 88-90 us per 4-step launch at N = 4, K = 2^20 against 98-100 on 512-element tiles (the
+  // body's 94 VGPRs leave 5 waves per SIMD, which only 4-wave workgroups fill;
+  // profiles/r05/p1, p2)
+  p->p_tile_width = 1;
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);
@@ -1377,6 +1382,10 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
   if (const char* v = std::getenv("DG_SWEEP_LANE_ELEMENTS")) {
     const int k = std::atoi(v);
     if (k == 2 || (k == 4 && p->NP <= 3)) p->sweep_lane_elems = k;
+  }
+  if (const char* v = std::getenv("DG_SNAP_PAIRS")) {
+    const int k = std::atoi(v);
+    if (k == 0 || k == 1) p->snap_pairs = k;
   }
   if (const char* v = std::getenv("DG_SWEEP_EXCHANGE")) {
     const int k = std::atoi(v);
@@ -1523,6 +1532,11 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       // removed in round 5 (item = workgroup id relied on in-order dispatch per XCD): only the
       // take counter (0) remains
       if (value != 0) return fail(DG_ERR_ARG, "sweep take: only 0 (the take counter) is supported");
+      return DG_OK;
+    case DG_TUNE_SNAP_PAIRS:
+      if (value != 0 && value != 1)
+        return fail(DG_ERR_ARG, "snapshot pairs: 0 (stage-loop kernels) or 1 (Horner pair tiles)");
+      p->snap_pairs = int(value);
       return DG_OK;
     case DG_TUNE_SWEEP_EXCHANGE:
       if (value != 0 && value != 1)
@@ -1691,6 +1705,24 @@ int dg_lserk4_fwd_ex(dg_plan* p, double* u, double t0, double dt, int nsteps, do
   std::vector<double> tn(size_t(nsteps) + 1);
   tn[0] = t0;
   for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  if (snapshots && p->snap_pairs && p->nstages == 5) {
+    // Horner-form pair tiles (k_step_rps): every state from the registers, the launch's last
+    // through LDS; u receives u^N by a copy when it is not snapshot 0
+    if (snapshots != u)
+      HIP_TRY(hipMemcpyAsync(snapshots, u, sizeof(double) * field, hipMemcpyDeviceToDevice, st));
+    for (int n = 0; n < nsteps;) {
+      int m = p->msteps;
+      while (m > nsteps - n) m >>= 1;
+      if (const int rc = pair_launch_step_snap(p, m, snapshots + int64_t(n) * field,
+                                               snapshots + int64_t(n + 1) * field, &tn[n], dt, st))
+        return rc;
+      n += m;
+    }
+    if (snapshots != u)
+      HIP_TRY(hipMemcpyAsync(u, snapshots + int64_t(nsteps) * field, sizeof(double) * field,
+                             hipMemcpyDeviceToDevice, st));
+    return DG_OK;
+  }
   if (snapshots) {
     if (snapshots != u)
       HIP_TRY(hipMemcpyAsync(snapshots, u, sizeof(double) * field, hipMemcpyDeviceToDevice, st));

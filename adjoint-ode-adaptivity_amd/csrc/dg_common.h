@@ -491,6 +491,10 @@ struct dg_plan {
   // Horner level (dg_rec_tiles.h), 1 overlapped waves: DPP within a wave, one LDS exchange and
   // barrier per step (dg_ovl_tiles.h)
   int sweep_exchange = 0;
+  // dg_lserk4_fwd with snapshots: 0 the stage-loop kernels (k_step / wave tiles; bit-identical
+  // to the record sweeps' stage-loop kernels), 1 Horner-form pair tiles (k_step_rps, dg_rec.hip;
+  // tiles of 512 * tile_width elements, msteps steps per launch)
+  int snap_pairs = 0;
   uint64_t* sweep_trace = nullptr;  // dg_plan_sweep_trace: per-item timestamps (profiling)
   int cu_count = 0;  // compute units of the plan's device (the dataflow grid)
   int xcd_order = 1;  // XCD-aware tile order
@@ -657,6 +661,10 @@ int sweep_err_word();
 // Jump-record sweep launches on pair tiles (dg_rec.hip), selected by plan->rec_lane_elems == 2.
 int pair_launch_step_rec(const dg_plan* p, int ms, const double* in, double* rec, double* last,
                          const double* times, double dt, hipStream_t st, int64_t n0, bool jend);
+// The snapshot forward on pair tiles (dg_rec.hip k_step_rps): ms steps from `in`, step st's
+// state into snap + st * field.
+int pair_launch_step_snap(const dg_plan* p, int ms, const double* in, double* snap,
+                          const double* times, double dt, hipStream_t st);
 int pair_launch_adj_rec(const dg_plan* p, int ms, const double* win, double* wout,
                         const double* rec, double* eta, int em, const double* t_next, double dt,
                         hipStream_t st, int64_t n0);

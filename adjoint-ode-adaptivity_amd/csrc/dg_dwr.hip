@@ -23,18 +23,9 @@
 // registers from the previous step, accumulates -w.R, and runs the 5 reverse stages.  No
 // prolonged field is ever stored: HBM sees the order-N snapshots once, w^{n0+MS} and w^{n0}
 // at order N+1, and eta.
-#include "dg_common.h"
+#include "dg_dwr_tiles.h"
 
 namespace dgk {
-
-// Prolongation in even/odd coordinates: e_hi = Pe e_lo, o_hi = Po o_lo.
-template <int NPL> struct PrEO {
-  static constexpr int NPH = NPL + 1;
-  static constexpr int NEL = (NPL + 1) / 2, NOL = NPL / 2;
-  static constexpr int NEH = (NPH + 1) / 2, NOH = NPH / 2;
-  double Pe[NEH * NEL];
-  double Po[NOH * NOL];
-};
 
 // Even/odd transform of an Np-node element (rows e_0..e_{NE-1}, o_0..o_{NO-1}) and its
 // inverse, as make_eo builds them (dg_common.h).
@@ -115,28 +106,6 @@ template <int NPL, int W> struct PGeo {
   static constexpr int kFaceD = 4 * (T + 2);  // two double-buffered face arrays, padded by 1
   static constexpr int kLds = kFB + kFaceD;
 };
-
-template <int NPL>
-__device__ __forceinline__ void prolong_eo(const double* __restrict__ u, const PrEO<NPL>& pr,
-                                           double* ev, double* od) {
-  using R = PrEO<NPL>;
-  double el[R::NEL], ol[R::NOL];
-  to_eo<NPL>(u, el, ol);
-#pragma unroll
-  for (int k = 0; k < R::NEH; ++k) {
-    double t = pr.Pe[k * R::NEL] * el[0];
-#pragma unroll
-    for (int j = 1; j < R::NEL; ++j) t = fma(pr.Pe[k * R::NEL + j], el[j], t);
-    ev[k] = t;
-  }
-#pragma unroll
-  for (int k = 0; k < R::NOH; ++k) {
-    double t = pr.Po[k * R::NOL] * ol[0];
-#pragma unroll
-    for (int j = 1; j < R::NOL; ++j) t = fma(pr.Po[k * R::NOL + j], ol[j], t);
-    od[k] = t;
-  }
-}
 
 template <int NPL, bool UNI, int W, int MS>
 __global__ __launch_bounds__(kBlock * W) void k_adj_p(const double* __restrict__ win,
@@ -433,12 +402,130 @@ int launch_adj_p_e(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, co
   return DG_OK;
 }
 
+// The Horner-form estimate (dg_dwr_tiles.h); the default since round 5 (DG_P_HORNER=0: round
+// 3's stage-loop kernel k_adj_p, for A/B runs).
+template <int NPL, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) void k_adj_ph(const double* __restrict__ win,
+                                                       double* __restrict__ wout,
+                                                       const double* __restrict__ snap,
+                                                       double* __restrict__ eta,
+                                                       const double* __restrict__ scale,
+                                                       AdjPHArgs<NPL, MS> args) {
+  using G = PHGeo<NPL, W>;
+  using A = AdjPHArgs<NPL, MS>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  constexpr int H = MS * 5;
+  const int64_t e0 = tile * (G::T - 2 * H) - H;
+  const DG_KAS A* ka =
+      reinterpret_cast<const DG_KAS A*>(kernarg_tail_k<decltype(&k_adj_ph<NPL, UNI, W, MS>), A>());
+  const double* kbnd = reinterpret_cast<const double*>(
+      kernarg_tail<decltype(&k_adj_ph<NPL, UNI, W, MS>), A>() + offsetof(A, bnd));
+  if (edge_tile(e0, G::T, args.ktot, args.K))
+    adjph_tile<NPL, UNI, W, MS, true>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd);
+  else
+    adjph_tile<NPL, UNI, W, MS, false>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd);
+}
+
+// The pipelined form (dg_dwr_tiles.h adjpq_tile): the forward recompute of step n-1 beside
+// the reverse step n, one barrier for both per level.
+// 4 waves per SIMD (<= 128 VGPRs) where the body is near it: 130 unconstrained at Np = 5
+template <int NPL> constexpr int kPQWaves = NPL <= 6 ? 4 : 1;
+
+template <int NPL, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) __attribute__((amdgpu_waves_per_eu(kPQWaves<NPL>))) void k_adj_pq(const double* __restrict__ win,
+                                                       double* __restrict__ wout,
+                                                       const double* __restrict__ snap,
+                                                       double* __restrict__ eta,
+                                                       const double* __restrict__ scale,
+                                                       AdjPHArgs<NPL, MS> args) {
+  using G = PQGeo<NPL, W>;
+  using A = AdjPHArgs<NPL, MS>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.xcd);
+  constexpr int H = MS * 5;
+  const int64_t e0 = tile * (G::T - 2 * H) - H;
+  const DG_KAS A* ka =
+      reinterpret_cast<const DG_KAS A*>(kernarg_tail_k<decltype(&k_adj_pq<NPL, UNI, W, MS>), A>());
+  const double* kbnd = reinterpret_cast<const double*>(
+      kernarg_tail<decltype(&k_adj_pq<NPL, UNI, W, MS>), A>() + offsetof(A, bnd));
+  if (edge_tile(e0, G::T, args.ktot, args.K))
+    adjpq_tile<NPL, UNI, W, MS, true>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd);
+  else
+    adjpq_tile<NPL, UNI, W, MS, false>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd);
+}
+
+inline int p_horner();
+
+template <int NPL, int W, int MS>
+int launch_adj_ph_e(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const double* win,
+                    double* wout, const double* snap, double* eta, int eta_mode,
+                    const double* tn, double dt, hipStream_t st, bool term) {
+  const dgr::RkPoly& P = dgr::rk_poly();
+  if (!P.ok) return fail(DG_ERR_HIP, "LSERK4 stability polynomial: beta_0 = beta_1 = 1 expected");
+  AdjPHArgs<NPL, MS> a;
+  make_eo<NPL + 1>(hi, hi->uniform ? dt * hi->s_uniform : 1.0, &a.op, true);
+  a.pr = pr;
+  a.sc = dt;
+  for (int k = 0; k < 6; ++k) a.beta[k] = P.beta[k];
+  double bnd[MS * 6 + 1];
+  dgr::rp_block_bnd(lo, MS, tn, dt, bnd);  // level weights of the MS steps (+ inflow values)
+  for (int i = 0; i < MS * 5; ++i) a.bnd[i] = bnd[i];
+  a.bnd[MS * 5] = 0.0;
+  a.ktot = lo->ktot;
+  a.stride = lo->ktot * NPL;
+  a.K = int32_t(lo->K);
+  a.has_eta = eta != nullptr ? (eta_mode | kEtaOn) : 0;
+  a.xcd = lo->xcd_order;
+  a.term = term ? 1 : 0;
+  constexpr int TE = kBlock * W - 2 * MS * 5;
+  const unsigned grid = grid_for(lo->ktot, TE);
+  if (p_horner() == 2) {
+    if (hi->uniform)
+      hipLaunchKernelGGL((k_adj_pq<NPL, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+                         wout, snap, eta, hi->d_scale, a);
+    else
+      hipLaunchKernelGGL((k_adj_pq<NPL, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+                         wout, snap, eta, hi->d_scale, a);
+  } else if (hi->uniform) {
+    hipLaunchKernelGGL((k_adj_ph<NPL, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+                       wout, snap, eta, hi->d_scale, a);
+  } else {
+    hipLaunchKernelGGL((k_adj_ph<NPL, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
+                       wout, snap, eta, hi->d_scale, a);
+  }
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+// DG_P_HORNER (read once, A/B runs): 0 round 3's stage loop (k_adj_p), 1 (default) Horner
+// (k_adj_ph), 2 Horner pipelined (k_adj_pq: the forward recompute of step n-1 beside the
+// reverse step n, half the barriers; 125 VGPRs, 4 waves per SIMD: measured 2-5 % slower than
+// k_adj_ph, profiles/r05/p3)
+inline int p_horner() {
+  static const int v = [] {
+    const char* e = std::getenv("DG_P_HORNER");
+    const int k = e ? std::atoi(e) : 1;
+    return (k == 0 || k == 2) ? k : 1;
+  }();
+  return v;
+}
+
 // Shapes: 256-element tiles with 1, 2 or 4 steps per launch; 512-element tiles with 2, 4 or 8.
 template <int NPL>
 int launch_adj_p_t(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, int ms,
                    const double* win, double* wout, const double* snap, double* eta, int em,
-                   const double* tn, double dt, hipStream_t st) {
+                   const double* tn, double dt, hipStream_t st, bool term) {
   const bool w2 = lo->p_tile_width == 2;
+  if (p_horner()) {
+    if (w2 && ms == 8) return launch_adj_ph_e<NPL, 2, 8>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st, term);
+    if (w2 && ms == 4) return launch_adj_ph_e<NPL, 2, 4>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st, term);
+    if (w2 && ms == 2) return launch_adj_ph_e<NPL, 2, 2>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st, term);
+    if (ms == 4) return launch_adj_ph_e<NPL, 1, 4>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st, term);
+    if (ms == 2) return launch_adj_ph_e<NPL, 1, 2>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st, term);
+    if (ms == 1) return launch_adj_ph_e<NPL, 1, 1>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st, term);
+    return fail(DG_ERR_ARG, "p-estimate: unsupported steps per launch for this tile width");
+  }
   if (w2 && ms == 8) return launch_adj_p_e<NPL, 2, 8>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
   if (w2 && ms == 4) return launch_adj_p_e<NPL, 2, 4>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
   if (w2 && ms == 2) return launch_adj_p_e<NPL, 2, 2>(lo, hi, pr, win, wout, snap, eta, em, tn, dt, st);
@@ -511,14 +598,22 @@ int dg_lserk4_adj_p(dg_plan* lo, dg_plan* hi, const double* P, double* w, const 
                     double t0, double dt, int nsteps, double* eta, int flags, void* stream) {
   if (!lo || !hi || !P || !w || !snapshots) return fail(DG_ERR_ARG, "null argument");
   if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
-  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS)) return fail(DG_ERR_ARG, "unknown flags");
+  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS | DG_ADJ_P_TERMINAL_PROLONG))
+    return fail(DG_ERR_ARG, "unknown flags");
+  bool term = (flags & DG_ADJ_P_TERMINAL_PROLONG) != 0;
   if (int rc = check_pair(lo, hi)) return rc;
   if (lo->NP > 8) return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (eta != nullptr && nsteps == 0 && (flags & DG_ADJ_ETA_ASSIGN))
     HIP_TRY(hipMemsetAsync(eta, 0, sizeof(double) * lo->ktot, st));
-  if (nsteps == 0) return DG_OK;
   const int64_t field_lo = lo->ktot * lo->NP, field_hi = hi->ktot * hi->NP;
+  if (term && (nsteps == 0 || p_horner() == 0)) {
+    // the round-3 kernel (and an empty sweep) take the terminal weight from w: form it first
+    if (const int rc = dg_prolong(lo, hi, P, snapshots + int64_t(nsteps) * field_lo, w, stream))
+      return rc;
+    term = false;
+  }
+  if (nsteps == 0) return DG_OK;
   std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt, as the forward sweep
   tn[0] = t0;
   for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
@@ -541,7 +636,8 @@ int dg_lserk4_adj_p(dg_plan* lo, dg_plan* hi, const double* P, double* w, const 
         PrEO<NPLV> pr;                                                                      \
         if (!make_prolong_eo<NPLV>(P, &pr))                                                 \
           return fail(DG_ERR_ARG, "P does not commute with the node reversal (symmetric nodes)"); \
-        rc = launch_adj_p_t<NPLV>(lo, hi, pr, m, in, out, snap, eta, em, &tn[n0], dt, st);   \
+        rc = launch_adj_p_t<NPLV>(lo, hi, pr, m, in, out, snap, eta, em, &tn[n0], dt, st,    \
+                                  term && l == 0);                                          \
       } break;
       DG_ADJP_CASE(2) DG_ADJP_CASE(3) DG_ADJP_CASE(4) DG_ADJP_CASE(5)
       DG_ADJP_CASE(6) DG_ADJP_CASE(7) DG_ADJP_CASE(8)

@@ -79,6 +79,72 @@ __global__ __launch_bounds__(64 * NW) void k_adj_rp(const double* __restrict__ w
                                                   os, args.n0);
 }
 
+// The snapshot forward on pair tiles (dg_lserk4_fwd with DG_TUNE_SNAP_PAIRS): MS steps of the
+// Horner-form body, every step's state stored (snap = u^{n0+1}, stride one field).
+template <int NP, bool UNI, int NW, int MS>
+__global__ __launch_bounds__(64 * NW) void k_step_rps(const double* __restrict__ uin,
+                                                         double* __restrict__ snap,
+                                                         const double* __restrict__ scale,
+                                                         RpStepArgs<NP, MS> args) {
+  using G = RpGeo<NP, NW, 2>;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 6 + 1];
+  const int64_t tile = tile_of(blockIdx.x, gridDim.x, args.c.xcd);
+  constexpr int H = RpHalo<MS>::F;
+  const int64_t e0 = tile * (G::T - 2 * H) - H;
+  using SArgs = RpStepArgs<NP, MS>;
+  const OpSrc<NP> os = op_src<NP>(
+      args.c, kernarg_tail_k<decltype(&k_step_rps<NP, UNI, NW, MS>), SArgs>() + offsetof(SArgs, c));
+  const int64_t field = args.c.ktot * NP;
+  double* last = snap + (MS - 1) * field;
+  if (edge_tile(e0, G::T, args.c.ktot, args.c.K)) {
+    const double* kb = reinterpret_cast<const double*>(
+        kernarg_tail<decltype(&k_step_rps<NP, UNI, NW, MS>), SArgs>() + offsetof(SArgs, bnd));
+    rp_step_tile<NP, UNI, NW, 2, MS, true, false, true>(lds, tile, uin, snap, last, scale, args.c,
+                                                        os, kb, 0, false, field);
+  } else {
+    rp_step_tile<NP, UNI, NW, 2, MS, false, false, true>(lds, tile, uin, snap, last, scale,
+                                                         args.c, os, nullptr, 0, false, field);
+  }
+}
+
+template <int NP, int NW, int MS>
+int rp_snap_e(const dg_plan* p, const double* in, double* snap, const double* times, double dt,
+              hipStream_t st) {
+  RpStepArgs<NP, MS> a;
+  if (const int rc = rp_make_op<NP>(p, dt, &a.c)) return rc;
+  rp_block_bnd(p, MS, times, dt, a.bnd);
+  a.n0 = 0;
+  a.jend = 0;
+  constexpr int TE = RpGeo<NP, NW, 2>::T - 2 * RpHalo<MS>::F;
+  const unsigned grid = grid_for(p->ktot, TE);
+  if (p->uniform)
+    hipLaunchKernelGGL((k_step_rps<NP, true, NW, MS>), dim3(grid), dim3(64 * NW), 0, st, in, snap,
+                       p->d_scale, a);
+  else
+    hipLaunchKernelGGL((k_step_rps<NP, false, NW, MS>), dim3(grid), dim3(64 * NW), 0, st, in,
+                       snap, p->d_scale, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+template <int NP>
+int rp_snap_np(const dg_plan* p, int ms, const double* in, double* snap, const double* times,
+               double dt, hipStream_t st) {
+  const bool w2 = p->tile_width == 2;
+  switch (ms) {
+    case 8: return w2 ? rp_snap_e<NP, 8, 8>(p, in, snap, times, dt, st)
+                      : rp_snap_e<NP, 4, 8>(p, in, snap, times, dt, st);
+    case 4: return w2 ? rp_snap_e<NP, 8, 4>(p, in, snap, times, dt, st)
+                      : rp_snap_e<NP, 4, 4>(p, in, snap, times, dt, st);
+    case 2: return w2 ? rp_snap_e<NP, 8, 2>(p, in, snap, times, dt, st)
+                      : rp_snap_e<NP, 4, 2>(p, in, snap, times, dt, st);
+    case 1: return w2 ? rp_snap_e<NP, 8, 1>(p, in, snap, times, dt, st)
+                      : rp_snap_e<NP, 4, 1>(p, in, snap, times, dt, st);
+    default: break;
+  }
+  return fail(DG_ERR_ARG, "pair snapshot forward: 1, 2, 4 or 8 steps per launch");
+}
+
 template <int NP, int NW, int E, int MS>
 int rp_step_e(const dg_plan* p, const double* in, double* rec, double* last, const double* times,
               double dt, hipStream_t st, int64_t n0, bool jend) {
@@ -189,6 +255,21 @@ int pair_launch_step_rec(const dg_plan* p, int ms, const double* in, double* rec
     case 7: return rp_step_np<7>(p, ms, in, rec, last, times, dt, st, n0, jend);
     case 8: return rp_step_np<8>(p, ms, in, rec, last, times, dt, st, n0, jend);
     case 9: return rp_step_np<9>(p, ms, in, rec, last, times, dt, st, n0, jend);
+    default: return fail(DG_ERR_ARG, "pair tiles support Np <= 9");
+  }
+}
+
+int pair_launch_step_snap(const dg_plan* p, int ms, const double* in, double* snap,
+                          const double* times, double dt, hipStream_t st) {
+  switch (p->NP) {
+    case 2: return rp_snap_np<2>(p, ms, in, snap, times, dt, st);
+    case 3: return rp_snap_np<3>(p, ms, in, snap, times, dt, st);
+    case 4: return rp_snap_np<4>(p, ms, in, snap, times, dt, st);
+    case 5: return rp_snap_np<5>(p, ms, in, snap, times, dt, st);
+    case 6: return rp_snap_np<6>(p, ms, in, snap, times, dt, st);
+    case 7: return rp_snap_np<7>(p, ms, in, snap, times, dt, st);
+    case 8: return rp_snap_np<8>(p, ms, in, snap, times, dt, st);
+    case 9: return rp_snap_np<9>(p, ms, in, snap, times, dt, st);
     default: return fail(DG_ERR_ARG, "pair tiles support Np <= 9");
   }
 }

@@ -393,13 +393,43 @@ __device__ __forceinline__ OpSrc<NP> op_src(const RpOp<NP>& rc, const DG_KAS cha
 // one face exchange of its input vector v (u at level 0, t after) through LDS.  `kb` (edge
 // tiles only): the block's rp_block_bnd constants in kernarg memory (lane-indexed reads);
 // lds must hold G::kLds + MS*6 + 1 doubles.
-template <int NP, bool UNI, int NW, int E, int MS, bool EDGE, bool WT>
+// Snapshot variant (SNAP, round 5: the snapshot forward on pair tiles, dg_lserk4_fwd with
+// DG_TUNE_SNAP_PAIRS): no record; `rec` is the launch's first output state u^{n0+1} and step st's
+// state u^{n0+st+1} is stored at rec + st * sstride straight from the registers (each lane's
+// two elements are 2 Np consecutive doubles), the last one through `last` as usual.
+template <int NP, int E, bool EDGE>
+__device__ __forceinline__ void rp_snap_put(double* __restrict__ g, const Elem* El,
+                                            const double (*ue)[(NP + 1) / 2],
+                                            const double (*uo)[NP / 2]) {
+  double v[E][NP];
+#pragma unroll
+  for (int m = 0; m < E; ++m) from_eo<NP>(ue[m], uo[m], v[m]);
+  const bool pair = El[0].valid && El[1].valid;
+  double* o = g + El[0].e * NP;
+  if (pair && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+      reinterpret_cast<double2*>(o)[q] = double2{v[(2 * q) / NP][(2 * q) % NP],
+                                                 v[(2 * q + 1) / NP][(2 * q + 1) % NP]};
+  } else {
+#pragma unroll
+    for (int m = 0; m < E; ++m)
+      if (El[m].valid) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i) g[El[m].e * NP + i] = v[m][i];
+      }
+  }
+}
+
+template <int NP, bool UNI, int NW, int E, int MS, bool EDGE, bool WT, bool SNAP = false>
 __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t tile,
                                              const double* __restrict__ uin,
                                              double* __restrict__ rec, double* __restrict__ last,
                                              const double* __restrict__ scale,
                                              const RpOp<NP>& c, OpSrc<NP> os,
-                                             const double* kb, int64_t n0, bool jend) {
+                                             const double* kb, int64_t n0, bool jend,
+                                             int64_t sstride = 0) {
+  static_assert(!SNAP || (E == 2 && !WT), "snapshots: launch chains on pair tiles");
   using G = RpGeo<NP, NW, E>;
   constexpr int T = G::T, LB = G::LB;
   constexpr int H = RpHalo<MS>::F;  // the level cone + the final state's neighbours, even
@@ -434,7 +464,8 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
     // u^{n0}'s left-face jumps (record n0-1) from the staged nodal values, as step_tile
     jv[m] = us[0] - ((EDGE && El[m].first) ? lds[CR] : us[-1]);
   }
-  if (n0 >= 1) rp_rec_put<E, EDGE, WT>(rec, n0 - 1, c.ktot, El, jv, ec);
+  if constexpr (!SNAP)
+    if (n0 >= 1) rp_rec_put<E, EDGE, WT>(rec, n0 - 1, c.ktot, El, jv, ec);
   __syncthreads();  // the image is read: the face arrays alias it
 
   const double b4 = c.beta[4], b5 = c.beta[5], b3 = c.beta[3], b2 = c.beta[2];
@@ -562,10 +593,13 @@ __device__ __forceinline__ void rp_step_tile(double* __restrict__ lds, int64_t t
           }
         }
       }
-      if (l == 0 && st >= 1) rp_rec_put<E, EDGE, WT>(rec, n0 + st - 1, c.ktot, El, jv, ec);
+      if constexpr (!SNAP)
+        if (l == 0 && st >= 1) rp_rec_put<E, EDGE, WT>(rec, n0 + st - 1, c.ktot, El, jv, ec);
     }
+    if constexpr (SNAP)
+      if (st < MS - 1) rp_snap_put<NP, E, EDGE>(rec + st * sstride, El, ue, uo);
   }
-  if (jend) {
+  if (!SNAP && jend) {
     // the sweep's final state u^{n0+MS}: one more face exchange for its jumps (record
     // n0+MS-1), inflow at t_{n0+MS}
     const int fL = ((MS * 5) & 1) * 2 * FB, fR = fL + FB;

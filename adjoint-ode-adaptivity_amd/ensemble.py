@@ -94,6 +94,11 @@ class EnsembleSweep:
         # at order N+1 from w = P u^N (J = |P u^N|^2 / 2 on the enriched nodes).
         self.est = DWREstimate(self.op)
         self.w = self.est.new_field()
+        if self.op.N >= 3:
+          # its forward keeps every state: the stage-loop step on pair tiles, 8 steps per
+          # launch on 1024-element tiles (84.4 us per launch, profiles/r05/p; the Horner-form
+          # pair step with register snapshot stores, snap_pairs=1, took 108.2 us)
+          self.op.tune(tile_width=2, steps_per_launch=8)
       else:
         # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
         # place on snapshot N (the library allows that alias) and leaves dJ/du^0 there.
@@ -120,17 +125,16 @@ class EnsembleSweep:
     self.run_adjoint()
 
   def terminal(self):
-    """The p-estimate's terminal weight w = P u^N (dg_prolong); nothing in the other modes
-    (their forward leaves u^N where the adjoint starts)."""
-    if self.est is not None:
-      self.est.prolong(self.snaps[self.nsteps], out=self.w)
+    """Nothing: the jump and snapshot modes' forward leaves u^N where the adjoint starts, and
+    the p-estimate's first adjoint launch forms its terminal weight w = P u^N from snapshot N
+    itself (DG_ADJ_P_TERMINAL_PROLONG, equal to dg_prolong into w first)."""
 
   def run_adjoint(self):
     """The adjoint kernels: w^N -> w^0 in place and eta = |DWR| per IC row (assigned, not
     accumulated: no zero fill needed)."""
     if self.est is not None:
       self.est.estimate(self.w, self.snaps, 0.0, self.dt, self.nsteps, eta=self.eta,
-                        eta_assign=True, eta_abs=True)
+                        eta_assign=True, eta_abs=True, terminal_prolong=True)
     elif self.record == "jumps":
       self.op.adjoint_rec(self.w, self.jumps, 0.0, self.dt, self.nsteps, eta=self.eta,
                           eta_assign=True, eta_abs=True)

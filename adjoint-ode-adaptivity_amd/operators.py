@@ -137,7 +137,8 @@ class DGAdvection1D:
   def tune(self, tile_width=None, steps_per_launch=None, xcd_order=None, lane_elements=None,
            rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
            rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None, rec_sweep=None,
-           sweep_waves=None, sweep_lane_elements=None, sweep_take=None, sweep_exchange=None):
+           sweep_waves=None, sweep_lane_elements=None, sweep_take=None, sweep_exchange=None,
+           snap_pairs=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -158,7 +159,10 @@ class DGAdvection1D:
     elements per lane of its tiles; ``sweep_take`` (0 / 1): its work items from one take
     counter or by workgroup id (bit-identical); ``sweep_exchange`` (0 / 1): its tiles exchange
     faces through LDS with a barrier per Horner level, or on overlapped waves by DPP with one
-    LDS exchange and barrier per step (tiles of waves * 116 + 12 elements; bit-identical)."""
+    LDS exchange and barrier per step (tiles of waves * 116 + 12 elements; bit-identical);
+    ``snap_pairs`` (0 / 1): ``forward`` with snapshots on the stage-loop kernels or on
+    Horner-form pair tiles (512 * ``tile_width`` elements, ``steps_per_launch`` steps per
+    launch; equal to rounding)."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
                      (_lib.DG_TUNE_REC_SWEEP, rec_sweep),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
@@ -168,7 +172,8 @@ class DGAdvection1D:
                      (_lib.DG_TUNE_SWEEP_WAVES, sweep_waves),
                      (_lib.DG_TUNE_SWEEP_LANE_ELEMENTS, sweep_lane_elements),
                      (_lib.DG_TUNE_SWEEP_TAKE, sweep_take),
-                     (_lib.DG_TUNE_SWEEP_EXCHANGE, sweep_exchange)):
+                     (_lib.DG_TUNE_SWEEP_EXCHANGE, sweep_exchange),
+                     (_lib.DG_TUNE_SNAP_PAIRS, snap_pairs)):
       if val is not None:
         _lib.check(self._lib.dg_plan_tune(self._plan, key, int(val)), "dg_plan_tune")
     if xcd_order is not None:
@@ -556,13 +561,19 @@ class DWREstimate:
     _lib.check(rc, "dg_prolong")
     return out
 
-  def estimate(self, w, snapshots, t0, dt, nsteps, eta=None, eta_assign=False, eta_abs=False):
+  def estimate(self, w, snapshots, t0, dt, nsteps, eta=None, eta_assign=False, eta_abs=False,
+               terminal_prolong=False):
     """The estimate over the sweep the lo plan's ``forward`` wrote into ``snapshots``
     ((nsteps+1) order-N fields): ``w`` (an order-(N+1) field, dJ_{N+1}/du at t_N) is swept
     back in place to t_0 and eta (batch*K) receives -sum_n w^{n+1} . R^n per element
-    (``eta_assign``: assign instead of accumulate; ``eta_abs``: store |eta|)."""
+    (``eta_assign``: assign instead of accumulate; ``eta_abs``: store |eta|).
+    ``terminal_prolong``: the terminal weight is P u^nsteps (J = |P u^N|^2 / 2), formed by the
+    first launch from the snapshot (w's input is not read; equal bit for bit to ``prolong``
+    into w first)."""
     eta_p = None if eta is None else self.lo._field(eta, "eta", self.lo.ktot)
-    flags = (_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) | (_lib.DG_ADJ_ETA_ABS if eta_abs else 0)
+    flags = ((_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) |
+             (_lib.DG_ADJ_ETA_ABS if eta_abs else 0) |
+             (_lib.DG_ADJ_P_TERMINAL_PROLONG if terminal_prolong else 0))
     rc = self.lo._lib.dg_lserk4_adj_p(
         self.lo._plan, self.hi._plan, self._P_ptr, self.hi._field(w, "w"),
         self.lo._field(snapshots, "snapshots", (nsteps + 1) * self.lo.field_numel),

@@ -107,7 +107,7 @@ PROFILE_DIRS = {
     "jumps": [os.path.join(ROOT, "profiles", "r05", d)
               for d in ("headline", "N1", "N2", "N6", "N8", "c4")],
     "snapshots": [os.path.join(ROOT, "profiles", "r02")],
-    "p": [os.path.join(ROOT, "profiles", "r04", "p")]}
+    "p": [os.path.join(ROOT, "profiles", "r05", "p")]}
 PROFILE_TRAFFIC_FILE = {"snapshots": "pmc_traffic_snapshots.json"}  # default pmc_traffic.json
 
 
@@ -524,7 +524,7 @@ def main_config3(args, world, rank, dev):
   # per launch, and the issued fp64 rate = the profile's issued flops per launch / this run's
   # launch time (every lane of a wave counted: halo lanes included).
   try:
-    with open(os.path.join(ROOT, "profiles", "r03", "config3", "pmc.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r05", "config3", "pmc.json")) as f:
       prof = json.load(f)
   except (OSError, ValueError):
     prof = None
@@ -715,7 +715,7 @@ def main(argv=None):
     if ev:
       ev[1].record(stream)
     if not args.graph:
-      sweep.terminal()  # the p-estimate's w = P u^N (dg_prolong); nothing otherwise
+      sweep.terminal()  # nothing (kept for the launch count; see EnsembleSweep.terminal)
     if ev:
       ev[3].record(stream)
     sweep.adjoint_graph() if args.graph else sweep.run_adjoint()

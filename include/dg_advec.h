@@ -139,19 +139,24 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             (tiles of waves * 116 + 12 elements on 8, 12 or 16 (Np <= 5)
  *                             waves; 20- or 10-step forward and 10-step adjoint blocks).
  *                             Bit-identical results
+ *   DG_TUNE_SNAP_PAIRS        dg_lserk4_fwd with snapshots: 0 (default) the stage-loop kernels
+ *                             (bit-identical to the record sweeps' stage loop), 1 the Horner-form
+ *                             step on pair tiles (512 * tile width elements, steps per launch as
+ *                             DG_TUNE_STEPS_PER_LAUNCH; equal to the stage loop to rounding)
  *   DG_TUNE_SWEEP_SPIN_LIMIT  diagnostics/tests: polls a dataflow work item makes before it
  *                             gives up waiting for a producer (0: the default, ~2^20; 1 makes
  *                             the watchdog fire on any multi-block sweep)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
  * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
- * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE. */
+ * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE, DG_SNAP_PAIRS. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
        DG_TUNE_P_TILE_WIDTH = 9, DG_TUNE_P_STEPS_PER_LAUNCH = 10,
        DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12,
        DG_TUNE_SWEEP_SPIN_LIMIT = 13, DG_TUNE_SWEEP_WAVES = 14,
-       DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16, DG_TUNE_SWEEP_EXCHANGE = 17 };
+       DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16, DG_TUNE_SWEEP_EXCHANGE = 17,
+       DG_TUNE_SNAP_PAIRS = 18 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
@@ -249,6 +254,10 @@ int dg_lserk4_adj(dg_plan* plan, double* w, const double* snapshots, double t0, 
  * decisions from it instead of re-testing every cell, and skips the limiter work and its
  * exchange in every stage where no cell of a tile is troubled (bit-identical results). */
 enum { DG_ADJ_ETA_ASSIGN = 1, DG_ADJ_ETA_ABS = 2 };
+/* dg_lserk4_adj_p only: the terminal weight is P u^nsteps (J = |P u^N|^2 / 2 on the enriched
+ * nodes), formed in the first launch from the snapshot it reads anyway; w's input is not read
+ * (the result equals dg_prolong into w first, bit for bit). */
+enum { DG_ADJ_P_TERMINAL_PROLONG = 8 };
 int dg_lserk4_adj_ex(dg_plan* plan, double* w, const double* snapshots, double t0, double dt,
                      int nsteps, double src_coef, double* eta, int flags,
                      const uint16_t* decisions, void* stream);
@@ -350,7 +359,8 @@ int dg_plan_sweep_trace(dg_plan* plan, uint64_t* trace);
  * dg_lserk4_adj_p:
  *   w (in/out, hi field): the terminal weight dJ_{N+1}/du on entry, w^0 on exit.
  *   snapshots: the (nsteps+1) order-N states dg_lserk4_fwd wrote (snapshots[n] = u^n).
- *   eta (nullable, batch*K) and flags as dg_lserk4_adj_ex (DG_ADJ_ETA_ASSIGN / _ABS).
+ *   eta (nullable, batch*K) and flags as dg_lserk4_adj_ex (DG_ADJ_ETA_ASSIGN / _ABS), plus
+ *   DG_ADJ_P_TERMINAL_PROLONG (w on entry := P u^nsteps, formed in the kernel).
  * Scratch: the hi plan's.  Neither plan may be used concurrently. */
 int dg_prolong(const dg_plan* lo, const dg_plan* hi, const double* P, const double* u,
                double* u_hi, void* stream);

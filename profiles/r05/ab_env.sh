@@ -6,7 +6,7 @@ args=$1; shift
 mkdir -p $out
 for rep in 1 2; do
   for e in "$@"; do
-    tag=$(echo "$e" | tr ' =' '__')
+    tag=$(echo "$e" | tr ' =/' '___')
     env $e timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-margin $args > $out/${tag}_$rep.json 2> $out/${tag}_$rep.err || { echo "bench $tag failed"; tail -20 $out/${tag}_$rep.err; exit 1; }
   done
 done
@@ -14,7 +14,7 @@ python - "$out" "$@" <<'PY'
 import json, sys
 out = sys.argv[1]
 for e in sys.argv[2:]:
-  tag = e.replace(" ", "_").replace("=", "_")
+  tag = e.replace(" ", "_").replace("=", "_").replace("/", "_")
   vals = []
   for rep in (1, 2):
     d = json.load(open(f"{out}/{tag}_{rep}.json"))

@@ -293,9 +293,39 @@ def test_full_size_p_estimate(pkg, gpu):
   1e-10 of max|oracle|, plus the refine index (numpy's argmax of |eta|).  The IC is a sine
   plus per-node noise so the residual is resolved (see test_gpu_full_size.py)."""
   out, est = run_case(pkg, gpu, 4, 1 << 20, 4, seed=21)
-  assert (est.tile_width, est.steps_per_launch) == (2, 4)  # the default launch shape
+  assert (est.tile_width, est.steps_per_launch) == (1, 4)  # the default launch shape (round 5)
   check(out)
   eta, eta_ref = out[0][0], out[0][1]
   a = np.sort(np.abs(eta_ref))
   assert a[-1] - a[-2] > 1e3 * RTOL * a[-1]
   assert int(np.argmax(np.abs(eta))) == int(np.argmax(np.abs(eta_ref)))
+
+
+@pytest.mark.parametrize("N,tw,spl", [(4, None, None), (2, 2, 4), (3, 1, 2)])
+def test_terminal_prolong_equals_prolong_first(pkg, gpu, N, tw, spl):
+  """DG_ADJ_P_TERMINAL_PROLONG (the bench's J = |P u^N|^2 / 2): the first launch forms
+  w = P u^N from the snapshot; w^0 and eta equal dg_prolong into w + the estimate bit for bit,
+  also on a batch with trajectory edges inside tiles."""
+  import torch
+  ops = pkg.operators
+  K, nsteps, batch = 700, 9, 2
+  v_x = np.linspace(0.0, 1.0, K + 1)
+  S = setup1d.startup1d(N, v_x, metric="element")
+  op = ops.DGAdvection1D(pkg.BaseGalerkin1D(n=N, v_x=v_x), a=A, batch=batch)
+  est = ops.DWREstimate(op, tile_width=tw, steps_per_launch=spl)
+  dt = oadv.bench_dt(S)
+  rng = np.random.default_rng(N)
+  u = dev(rng.standard_normal(batch * K * (N + 1)), gpu)
+  snaps = op.new_field(nsteps + 1)
+  op.forward(u, 0.0, dt, nsteps, snaps)
+  w_ref = est.new_field()
+  est.prolong(snaps[nsteps], out=w_ref)
+  eta_ref = torch.empty(batch * K, dtype=torch.float64, device=gpu)
+  est.estimate(w_ref, snaps, 0.0, dt, nsteps, eta=eta_ref, eta_assign=True, eta_abs=True)
+  w = torch.full_like(w_ref, float("nan"))  # not read
+  eta = torch.empty_like(eta_ref)
+  est.estimate(w, snaps, 0.0, dt, nsteps, eta=eta, eta_assign=True, eta_abs=True,
+               terminal_prolong=True)
+  torch.cuda.synchronize()
+  np.testing.assert_array_equal(host(w), host(w_ref))
+  np.testing.assert_array_equal(host(eta), host(eta_ref))

@@ -508,3 +508,59 @@ def test_ensemble_per_ic_rows_and_gather(pkg, gpu):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(host(rows[b]), host(one.eta))
   assert torch.equal(pkg.ensemble.gather_per_ic(rows, 3), rows)
+
+
+@pytest.mark.parametrize("N,K,tw,ms,nsteps,refined", [
+    (4, 3000, 2, 8, 20, False),   # the p-estimate bench's forward shape: 8 + 8 + 4 launches
+    (4, 1000, 1, 4, 7, False),    # 512-element tiles, 4 + 2 + 1
+    (1, 2000, 2, 8, 9, False),
+    (2, 777, 1, 2, 5, True),
+    (6, 1500, 2, 4, 6, True),
+    (8, 900, 2, 8, 8, False),
+    (3, 100, 2, 8, 3, False),     # fewer elements than one tile's output
+])
+def test_snapshot_forward_on_pair_tiles(pkg, gpu, N, K, tw, ms, nsteps, refined):
+  """DG_TUNE_SNAP_PAIRS = 1: the snapshot forward as the Horner-form step on pair tiles
+  (k_step_rps), every snapshot and u^N against the oracle's LSERK4 loop at 1e-10."""
+  import torch
+  rng = np.random.default_rng(N + 7)
+  v_x = None
+  if refined:
+    v_x = np.concatenate(([0.0], np.cumsum(rng.uniform(0.5, 1.5, K))))
+    v_x = v_x / v_x[-1]
+  S, mesh = mesh_pair(pkg, N, K, v_x=v_x)
+  u0 = np.sin(2 * np.pi * S["x"]) + 0.1 * rng.standard_normal(S["x"].shape)
+  dt = oadv.bench_dt(S)
+  ref, _ = oadv.forward_sweep(u0, 0.05, dt, nsteps, A, S)
+  op = make_op(pkg, mesh)
+  op.tune(tile_width=tw, steps_per_launch=ms, snap_pairs=1)
+  u = dev(setup1d.to_elem_major(u0), gpu)
+  snaps = op.new_field(nsteps + 1)
+  op.forward(u, 0.05, dt, nsteps, snaps)
+  torch.cuda.synchronize()
+  for n in range(nsteps + 1):
+    assert rel_err(setup1d.from_elem_major(host(snaps[n]), N + 1), ref[n]) <= RTOL, n
+  assert rel_err(setup1d.from_elem_major(host(u), N + 1), ref[-1]) <= RTOL
+
+
+def test_snapshot_forward_pairs_batch_edges(pkg, gpu):
+  """Pair-tile snapshots of a batch (trajectory edges inside tiles, odd Np * ktot so the
+  snapshot stride is not 16-byte aligned) equal the stage-loop kernels' to rounding."""
+  import torch
+  N, K, batch, nsteps = 4, 1001, 3, 10
+  S, mesh = mesh_pair(pkg, N, K)
+  op = make_op(pkg, mesh, batch=batch, inflow="a2")
+  rng = np.random.default_rng(5)
+  u0 = dev(rng.standard_normal(batch * K * (N + 1)), gpu)
+  dt = oadv.bench_dt(S)
+  out = []
+  for pairs in (0, 1):
+    op.tune(tile_width=2, steps_per_launch=8 if pairs else 4, snap_pairs=pairs)
+    snaps = op.new_field(nsteps + 1)
+    u = u0.clone()
+    op.forward(u, 0.0, dt, nsteps, snaps)
+    torch.cuda.synchronize()
+    out.append(host(snaps))
+  assert np.all(np.isfinite(out[1]))
+  for n in range(nsteps + 1):
+    assert rel_err(out[1][n], out[0][n]) <= 1e-12, n
