@@ -1208,6 +1208,9 @@ bool sweep_shape(const dg_plan* p, int nsteps, int* waves, int* msf, int* msa) {
 // partials).  Grows the control region to `sync_bytes` (zeroing what it newly covers, which
 // an earlier call may have used as data) and the allocation to hold `data_bytes` after it.
 // *data = the data region's start.
+}  // namespace
+
+namespace dgk {
 int sweep_scratch(dg_plan* p, size_t sync_bytes, size_t data_bytes, hipStream_t st, char** data) {
   const size_t sync = sync_bytes > p->sweep_sync ? sync_bytes : p->sweep_sync;
   if (!p->d_sweep || p->sweep_bytes < sync + data_bytes) {
@@ -1234,7 +1237,25 @@ int sweep_scratch(dg_plan* p, size_t sync_bytes, size_t data_bytes, hipStream_t 
   *data = static_cast<char*>(p->d_sweep) + sync;
   return DG_OK;
 }
-}  // namespace
+
+// The dataflow launches' watchdog: fails if an earlier launch of the plan gave up (until
+// dg_sweep_status clears the flag), and maps the host-visible flag on first use.
+int sweep_watchdog(dg_plan* p) {
+  if (p->h_sweep_err && *static_cast<volatile uint32_t*>(p->h_sweep_err) != 0u)
+    return fail(DG_ERR_HIP, "a dataflow sweep of this plan gave up waiting for a producer (its "
+                            "outputs were poisoned with NaN); dg_sweep_status clears the flag");
+  if (!p->h_sweep_err) {  // mapped page-locked memory
+    void* h = nullptr;
+    HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
+    p->h_sweep_err = static_cast<uint32_t*>(h);
+    *p->h_sweep_err = 0u;
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
+    p->d_sweep_err = static_cast<uint32_t*>(d);
+  }
+  return DG_OK;
+}
+}  // namespace dgk
 
 // ---------------------------------------------------------------------------
 // C ABI
@@ -1374,6 +1395,10 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
       const int k = std::atoi(v);
       if (k == 1 || k == 2 || k == 4 || k == 8) p->p_msteps = k;
     }
+  if (const char* v = std::getenv("DG_P_FLOW")) {
+    const int k = std::atoi(v);
+    if (k == 0 || k == 1) p->p_flow = k;
+  }
   }
   if (const char* v = std::getenv("DG_REC_SWEEP")) {
     const int k = std::atoi(v);
@@ -1532,6 +1557,11 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       // removed in round 5 (item = workgroup id relied on in-order dispatch per XCD): only the
       // take counter (0) remains
       if (value != 0) return fail(DG_ERR_ARG, "sweep take: only 0 (the take counter) is supported");
+      return DG_OK;
+    case DG_TUNE_P_FLOW:
+      if (value != 0 && value != 1)
+        return fail(DG_ERR_ARG, "p-estimate flow: 0 (one launch per block) or 1 (one dataflow launch)");
+      p->p_flow = int(value);
       return DG_OK;
     case DG_TUNE_SNAP_PAIRS:
       if (value != 0 && value != 1)
@@ -1936,18 +1966,7 @@ int sweep_rec_impl(dg_plan* p, const double* u0, double* uN, double* w, double* 
       return rc;
     return idx ? dg_argmax_ex(p, eta, p->ktot, 1, idx, value, nonfinite, stream) : DG_OK;
   }
-  if (p->h_sweep_err && *static_cast<volatile uint32_t*>(p->h_sweep_err) != 0u)
-    return fail(DG_ERR_HIP, "a dataflow sweep of this plan gave up waiting for a producer (its "
-                            "outputs were poisoned with NaN); dg_sweep_status clears the flag");
-  if (!p->h_sweep_err) {  // the watchdog's host-visible flag, mapped page-locked memory
-    void* h = nullptr;
-    HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
-    p->h_sweep_err = static_cast<uint32_t*>(h);
-    *p->h_sweep_err = 0u;
-    void* d = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
-    p->d_sweep_err = static_cast<uint32_t*>(d);
-  }
+  if (const int rc = sweep_watchdog(p)) return rc;
   const int nbF = nsteps / msf, nbA = nsteps / msa;
   const int64_t items = sweep_items(p, waves, msf, msa, nsteps);
   // The scratch is sized for the plan's reserved capacity (K_cap elements per trajectory), so

@@ -456,6 +456,9 @@ struct dg_plan {
   // 512 elements), steps per launch 1, 2, 4 or 8 (8 on 512-element tiles)
   int p_tile_width = 2;
   int p_msteps = 4;
+  // 1: the estimate runs as ONE dataflow launch (k_adjp_flow) when its steps split into >= 2
+  // blocks of p_msteps; 0: one launch per block
+  int p_flow = 0;
   // the dataflow sweep (dg_lserk4_sweep_rec, dg_sweep.hip): its scratch (sync words, block
   // states, indicator partials; grown on demand) and the switch (1: one dataflow launch where
   // the shape allows it, 0: the launch-per-block pair)
@@ -656,6 +659,11 @@ int sweep_launch_rec(dg_plan* p, int waves, int msf, int msa, const SweepBufs& b
                      double dt, int nsteps, int mode, hipStream_t st);
 int sweep_sync_words();
 int sweep_max_steps();
+// The plan's dataflow scratch (dg_advec.hip): a control region of `sync_bytes` (zeroed where
+// newly covered) followed by `data_bytes`; *data = the data region.
+int sweep_scratch(dg_plan* p, size_t sync_bytes, size_t data_bytes, hipStream_t st, char** data);
+// Fails if an earlier dataflow launch of the plan gave up; maps the watchdog's host flag.
+int sweep_watchdog(dg_plan* p);
 int sweep_err_word();
 
 // Jump-record sweep launches on pair tiles (dg_rec.hip), selected by plan->rec_lane_elems == 2.

@@ -24,6 +24,7 @@
 // prolonged field is ever stored: HBM sees the order-N snapshots once, w^{n0+MS} and w^{n0}
 // at order N+1, and eta.
 #include "dg_dwr_tiles.h"
+#include "dg_flow.h"
 
 namespace dgk {
 
@@ -404,7 +405,7 @@ int launch_adj_p_e(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, co
 
 // The Horner-form estimate (dg_dwr_tiles.h); the default since round 5 (DG_P_HORNER=0: round
 // 3's stage-loop kernel k_adj_p, for A/B runs).
-template <int NPL, bool UNI, int W, int MS>
+template <int NPL, bool UNI, int W, int MS, bool GL>
 __global__ __launch_bounds__(kBlock * W) void k_adj_ph(const double* __restrict__ win,
                                                        double* __restrict__ wout,
                                                        const double* __restrict__ snap,
@@ -418,13 +419,15 @@ __global__ __launch_bounds__(kBlock * W) void k_adj_ph(const double* __restrict_
   constexpr int H = MS * 5;
   const int64_t e0 = tile * (G::T - 2 * H) - H;
   const DG_KAS A* ka =
-      reinterpret_cast<const DG_KAS A*>(kernarg_tail_k<decltype(&k_adj_ph<NPL, UNI, W, MS>), A>());
+      reinterpret_cast<const DG_KAS A*>(kernarg_tail_k<decltype(&k_adj_ph<NPL, UNI, W, MS, GL>), A>());
   const double* kbnd = reinterpret_cast<const double*>(
-      kernarg_tail<decltype(&k_adj_ph<NPL, UNI, W, MS>), A>() + offsetof(A, bnd));
+      kernarg_tail<decltype(&k_adj_ph<NPL, UNI, W, MS, GL>), A>() + offsetof(A, bnd));
   if (edge_tile(e0, G::T, args.ktot, args.K))
-    adjph_tile<NPL, UNI, W, MS, true>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd);
+    adjph_tile<NPL, UNI, W, MS, true, GL>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd,
+                                          args.term != 0);
   else
-    adjph_tile<NPL, UNI, W, MS, false>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd);
+    adjph_tile<NPL, UNI, W, MS, false, GL>(lds, tile, win, wout, snap, eta, scale, args, ka, kbnd,
+                                           args.term != 0);
 }
 
 // The pipelined form (dg_dwr_tiles.h adjpq_tile): the forward recompute of step n-1 beside
@@ -487,13 +490,243 @@ int launch_adj_ph_e(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, c
     else
       hipLaunchKernelGGL((k_adj_pq<NPL, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
                          wout, snap, eta, hi->d_scale, a);
+  } else if (p_horner() == 3) {
+    if (hi->uniform)
+      hipLaunchKernelGGL((k_adj_ph<NPL, true, W, MS, true>), dim3(grid), dim3(kBlock * W), 0, st,
+                         win, wout, snap, eta, hi->d_scale, a);
+    else
+      hipLaunchKernelGGL((k_adj_ph<NPL, false, W, MS, true>), dim3(grid), dim3(kBlock * W), 0, st,
+                         win, wout, snap, eta, hi->d_scale, a);
   } else if (hi->uniform) {
-    hipLaunchKernelGGL((k_adj_ph<NPL, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
-                       wout, snap, eta, hi->d_scale, a);
+    hipLaunchKernelGGL((k_adj_ph<NPL, true, W, MS, false>), dim3(grid), dim3(kBlock * W), 0, st,
+                       win, wout, snap, eta, hi->d_scale, a);
   } else {
-    hipLaunchKernelGGL((k_adj_ph<NPL, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, win,
-                       wout, snap, eta, hi->d_scale, a);
+    hipLaunchKernelGGL((k_adj_ph<NPL, false, W, MS, false>), dim3(grid), dim3(kBlock * W), 0, st,
+                       win, wout, snap, eta, hi->d_scale, a);
   }
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// The estimate as ONE dataflow launch (k_adjp_flow; plan->p_flow, dg_plan_tune
+// DG_TUNE_P_FLOW).  The launch-per-block chain pays each launch's fill and drain: at K = 2^20,
+// Np = 5 a 4-step launch is 4,855 tiles of 17-us workgroups over 1,536 resident slots, and the
+// SQ counters put the average residency at 4.3 of 6 waves per SIMD (profiles/r05/p_gl_w1).
+// Here the blocks' tiles are the work items of one launch, in queue order block 0 (the last
+// MS steps) tiles 0..nT-1, block 1, ...; item (b, j) waits for (b-1, j-1..j+1), whose outputs
+// cover its input range (halo < TE).  The hand-off protocol, the take counter, the watchdog
+// and the poisoning are the jump sweep's (dg_sweep_kernel.h, dg_flow.h): w is handed off
+// write-through and loaded sc1; each block but the last writes its indicator partials to its
+// own row and the last adds them in launch order (bit-identical to the chain); the fused
+// refine decision (dg_lserk4_adj_p_refine) reduces the last block's tile winners.  The
+// snapshots come from an earlier launch: plain loads (and direct-to-LDS, GL).
+// ---------------------------------------------------------------------------
+template <int NPL, int MS> struct AdjPFArgs {
+  static constexpr int kMaxBlocks = dgr::kSweepMaxSteps / MS;
+  EOArgs<NPL + 1> op;
+  PrEO<NPL> pr;
+  double sc;
+  double beta[6];
+  double bnd[kMaxBlocks * (MS * 5 + 1)];  // block b's level weights at b (5 MS + 1), then a 0
+  const double* snap;                    // u^0 .. u^nsteps, `stride` doubles apart
+  double* W[kMaxBlocks + 1];             // block b reads W[b] (W[0]: terminal weight), writes W[b+1]
+  double* eta;
+  double* part;                          // (nb - 1) rows of ktot: the blocks' partial indicators
+  const double* scale;
+  uint32_t* sync;                        // kSync* words, then one flag per item
+  uint32_t* err_host;
+  uint64_t* trace;                       // nullable: per item {dequeued, producers done,
+                                         // published, XCC id << 32 | workgroup id}
+  int64_t* am_idx;                       // nullable: the fused refine decision
+  double* am_val;
+  int64_t* am_nf;
+  double* am_pv;                         // per last-block tile: its (|eta|, element) winner
+  int64_t* am_pi;
+  int64_t ktot;
+  int64_t stride;
+  int32_t K;
+  int32_t has_eta;                       // kEta* bits of the whole sweep
+  int32_t term;                          // block 0's terminal weight is P u^nsteps
+  int32_t nb, nT, nsteps, spin_limit;
+};
+
+// 6 waves per SIMD (<= 80 VGPRs, as k_adj_ph<..., GL> compiles unconstrained) where the body
+// fits: the item decode and the indicator sink would otherwise take it to 100 at Np = 5.
+template <int NPL, bool UNI> constexpr int kPFWaves = (UNI && NPL <= 5) ? 6 : 1;
+
+template <int NPL, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) __attribute__((amdgpu_waves_per_eu(kPFWaves<NPL, UNI>)))
+void k_adjp_flow(AdjPFArgs<NPL, MS> a) {
+  using G = PHGeo<NPL, W>;
+  using A = AdjPFArgs<NPL, MS>;
+  constexpr int NPH = NPL + 1, H = MS * 5, TE = G::T - 2 * H, NW = kBlock * W / 64;
+  __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
+  __shared__ uint32_t s_item, s_epoch, s_last, s_bad;
+  __shared__ double s_av[NW];
+  __shared__ int64_t s_ai[NW];
+  uint32_t* sync = a.sync;
+  uint32_t* flags = sync + dgr::kSyncFlags;
+  const int tid = threadIdx.x;
+  const int nT = a.nT, nb = a.nb;
+  if (tid == 0) {
+    uint32_t it, ep;
+    dgr::flow_take(sync, int64_t(nb) * nT, &it, &ep);
+    s_item = it;
+    s_epoch = ep;
+    s_bad = 0u;
+  }
+  __syncthreads();
+  const int64_t item = s_item;
+  const uint32_t epoch = s_epoch;
+  const uint64_t t_deq = a.trace ? uint64_t(wall_clock64()) : 0;
+  uint64_t t_ready = 0;
+  const int blk = int(item / nT), j = int(item - int64_t(blk) * nT);
+  // the poll of the previous block's tiles j-1..j+1, run by the tile body once its snapshot
+  // loads are in flight
+  const auto wait_inputs = [&]() {
+    if (blk > 0 && tid < 64) {
+      const int lo = j > 0 ? j - 1 : 0, hi = j + 1 < nT ? j + 1 : nT - 1;
+      const bool gave_up = dgr::sweep_wait(flags + int64_t(blk - 1) * nT + lo, hi - lo + 1,
+                                           epoch, sync, a.err_host, a.spin_limit);
+      if (tid == 0 && gave_up) s_bad = 1u;
+    }
+    // no acquire fence: every load of handed-off bytes is an sc1 load; this only keeps the
+    // compiler from hoisting them above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    if (a.trace) t_ready = uint64_t(wall_clock64());
+  };
+  const DG_KAS A* ka =
+      reinterpret_cast<const DG_KAS A*>(kernarg_tail_k<decltype(&k_adjp_flow<NPL, UNI, W, MS>), A>());
+  const double* kbnd = reinterpret_cast<const double*>(
+                           kernarg_tail<decltype(&k_adjp_flow<NPL, UNI, W, MS>), A>() +
+                           offsetof(A, bnd)) + blk * (MS * 5 + 1);
+  const int64_t ktot = a.ktot;
+  const int64_t n0 = int64_t(a.nsteps) - int64_t(blk + 1) * MS;
+  const bool lastb = blk == nb - 1;
+  dgr::EtaSink es;
+  es.eta = a.eta;
+  es.part_out = (a.has_eta && !lastb) ? a.part + int64_t(blk) * ktot : nullptr;
+  es.part_in = a.part;
+  es.part_ld = ktot;
+  es.nparts = lastb ? nb - 1 : 0;
+  es.mode = a.has_eta;
+  es.argmax = lastb && a.am_idx != nullptr;
+  es.bv = -INFINITY;  // the weakest candidate (dg_argmax's convention)
+  es.bi = INT64_MAX;
+  const double* snap = a.snap + n0 * a.stride;
+  const bool term = a.term != 0 && blk == 0;
+  const int64_t e0 = int64_t(j) * TE - H;
+  if (edge_tile(e0, G::T, ktot, a.K))
+    adjph_tile<NPL, UNI, W, MS, true, true, true, A>(lds, j, a.W[blk], a.W[blk + 1], snap, a.eta,
+                                                     a.scale, a, ka, kbnd, term, &es,
+                                                     wait_inputs);
+  else
+    adjph_tile<NPL, UNI, W, MS, false, true, true, A>(lds, j, a.W[blk], a.W[blk + 1], snap,
+                                                      a.eta, a.scale, a, ka, kbnd, term, &es,
+                                                      wait_inputs);
+  if (s_bad) {
+    // the body's own write-through stores (another lane mapping) complete first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int64_t o0 = int64_t(j) * TE, ndh = ktot * NPH;
+    const int64_t ne = (ktot - o0) < TE ? ktot - o0 : int64_t(TE);
+    dgr::poison_run<kBlock * W>(a.W[blk + 1], o0 * NPH,
+                                (ndh - o0 * NPH) < int64_t(TE) * NPH ? ndh - o0 * NPH
+                                                                     : int64_t(TE) * NPH);
+    if (a.has_eta) dgr::poison_run<kBlock * W>(es.part_out ? es.part_out : a.eta, o0, ne);
+    es.bv = __builtin_nan("");
+  }
+  if (es.argmax) {  // the tile's winner, a hand-off to the last arriving tile
+    dgr::wg_argmax<NW>(es.bv, es.bi, s_av, s_ai);
+    if (tid == 0) {
+      dgr::st8_agent(a.am_pv + j, __builtin_bit_cast(uint64_t, es.bv));
+      dgr::st8_agent(a.am_pi + j, uint64_t(es.bi));
+    }
+  }
+  // publish: every wave's write-through stores have completed, then one flag store
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) dgr::st_agent(flags + item, epoch);
+  if (es.argmax)
+    dgr::flow_refine_arrive<NW>(sync, nT, a.am_pv, a.am_pi, a.am_idx, a.am_val, a.am_nf, &s_last,
+                                s_av, s_ai);
+  if (a.trace && tid == 0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* tr = a.trace + 4 * item;
+    tr[0] = t_deq;
+    tr[1] = t_ready;
+    tr[2] = uint64_t(wall_clock64());
+    tr[3] = (uint64_t(xcc) << 32) | blockIdx.x;
+  }
+}
+
+// Buffers of one k_adjp_flow launch (dg_lserk4_adj_p's scratch on the order-N plan).
+struct PFlowBufs {
+  double* W[dgr::kSweepMaxSteps + 1];
+  double* part;
+  uint32_t* sync;
+  int64_t* am_idx;
+  double* am_val;
+  int64_t* am_nf;
+  double* am_pv;
+  int64_t* am_pi;
+};
+
+template <int NPL, int W, int MS>
+int launch_adjp_flow(dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const PFlowBufs& b,
+                     const double* snapshots, double* eta, int mode, const double* tn, double dt,
+                     int nsteps, bool term, hipStream_t st) {
+  const dgr::RkPoly& P = dgr::rk_poly();
+  if (!P.ok) return fail(DG_ERR_HIP, "LSERK4 stability polynomial: beta_0 = beta_1 = 1 expected");
+  using A = AdjPFArgs<NPL, MS>;
+  const int nb = nsteps / MS;
+  if (nb < 2 || nb > A::kMaxBlocks || nb * MS != nsteps)
+    return fail(DG_ERR_ARG, "p-estimate dataflow: nsteps must be 2..40/MS blocks of MS steps");
+  A a;
+  make_eo<NPL + 1>(hi, hi->uniform ? dt * hi->s_uniform : 1.0, &a.op, true);
+  a.pr = pr;
+  a.sc = dt;
+  for (int k = 0; k < 6; ++k) a.beta[k] = P.beta[k];
+  for (int bk = 0; bk < nb; ++bk) {  // block b covers steps n0 .. n0+MS-1, n0 = nsteps - (b+1) MS
+    const int n0 = nsteps - (bk + 1) * MS;
+    double bnd[MS * 6 + 1];
+    dgr::rp_block_bnd(lo, MS, &tn[n0], dt, bnd);
+    double* row = a.bnd + bk * (MS * 5 + 1);
+    for (int i = 0; i < MS * 5; ++i) row[i] = bnd[i];
+    row[MS * 5] = 0.0;
+  }
+  for (int bk = nb; bk < A::kMaxBlocks; ++bk)
+    for (int i = 0; i <= MS * 5; ++i) a.bnd[bk * (MS * 5 + 1) + i] = 0.0;
+  a.snap = snapshots;
+  for (int i = 0; i <= A::kMaxBlocks; ++i) a.W[i] = i <= nb ? b.W[i] : nullptr;
+  a.eta = eta;
+  a.part = b.part;
+  a.scale = hi->d_scale;
+  a.sync = b.sync;
+  a.err_host = lo->d_sweep_err;
+  a.trace = lo->sweep_trace;
+  a.am_idx = b.am_idx;
+  a.am_val = b.am_val;
+  a.am_nf = b.am_nf;
+  a.am_pv = b.am_pv;
+  a.am_pi = b.am_pi;
+  a.ktot = lo->ktot;
+  a.stride = lo->ktot * NPL;
+  a.K = int32_t(lo->K);
+  a.has_eta = mode;
+  a.term = term ? 1 : 0;
+  a.nb = nb;
+  a.nT = int(grid_for(lo->ktot, kBlock * W - 2 * MS * 5));
+  a.nsteps = nsteps;
+  a.spin_limit = lo->sweep_spin_limit > 0 ? lo->sweep_spin_limit : dgr::kSweepSpinLimit;
+  const unsigned grid = unsigned(int64_t(nb) * a.nT);
+  if (hi->uniform)
+    hipLaunchKernelGGL((k_adjp_flow<NPL, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_adjp_flow<NPL, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, a);
   HIP_TRY(hipGetLastError());
   return DG_OK;
 }
@@ -501,12 +734,13 @@ int launch_adj_ph_e(const dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, c
 // DG_P_HORNER (read once, A/B runs): 0 round 3's stage loop (k_adj_p), 1 (default) Horner
 // (k_adj_ph), 2 Horner pipelined (k_adj_pq: the forward recompute of step n-1 beside the
 // reverse step n, half the barriers; 125 VGPRs, 4 waves per SIMD: measured 2-5 % slower than
-// k_adj_ph, profiles/r05/p3)
+// k_adj_ph, profiles/r05/p3), 3 Horner with the snapshot tiles loaded straight into LDS
+// (k_adj_ph<..., GL = true>: no prefetch registers)
 inline int p_horner() {
   static const int v = [] {
     const char* e = std::getenv("DG_P_HORNER");
     const int k = e ? std::atoi(e) : 1;
-    return (k == 0 || k == 2) ? k : 1;
+    return (k == 0 || k == 2 || k == 3) ? k : 1;
   }();
   return v;
 }
@@ -565,6 +799,157 @@ int check_pair(const dg_plan* lo, const dg_plan* hi) {
   return DG_OK;
 }
 
+// The dataflow form applies: the plan asks for it, the Horner kernels are selected, and the
+// steps split into 2 .. 40/MS blocks of the plan's steps per launch (4 on 256-element tiles;
+// 4 or 8 on 512-element tiles).
+bool p_flow_shape(const dg_plan* lo, int nsteps) {
+  const int m = p_msteps(lo);
+  const int h = p_horner();
+  return lo->p_flow && (h == 1 || h == 3) && (m == 4 || (m == 8 && lo->p_tile_width == 2)) &&
+         nsteps > 0 && nsteps % m == 0 && nsteps / m >= 2 && nsteps <= dgr::kSweepMaxSteps;
+}
+
+// One dataflow launch of the whole estimate (k_adjp_flow).  Scratch: the lo plan's dataflow
+// region (sweep_scratch: control words, then the blocks' w outputs W[1..nb-1] and partial
+// indicator rows, sized for the reserved capacity).  W[0] = W[nb] = w: the first block reads
+// it (unless the terminal weight is formed in the kernel) and the last rewrites it; with
+// nb >= 2 the last block's tile j starts after every first-block tile whose input range
+// overlaps its output range (j-1..j+1, through the chain of waits).
+int adjp_flow(dg_plan* lo, const dg_plan* hi, const double* P, double* w,
+              const double* snapshots, const double* tn, double dt, int nsteps, double* eta,
+              int mode, bool term, int64_t* idx, double* value, int64_t* nonfinite,
+              hipStream_t st) {
+  if (const int rc = sweep_watchdog(lo)) return rc;
+  const int m = p_msteps(lo), nb = nsteps / m, W = lo->p_tile_width;
+  const int64_t TE = int64_t(kBlock) * W - 10 * m;
+  const int64_t nT = (lo->ktot + TE - 1) / TE, items = int64_t(nb) * nT;
+  const int64_t kcap = lo->K_cap * lo->batch;
+  const int64_t nT_cap = (kcap + TE - 1) / TE, items_cap = int64_t(nb) * nT_cap;
+  const size_t sync_bytes =
+      (sizeof(uint32_t) * size_t(sweep_sync_words() + items_cap) + 255) & ~size_t(255);
+  const int64_t field_hi = lo->ktot * hi->NP;
+  const size_t fcap = sizeof(double) * size_t(kcap) * size_t(hi->NP);
+  const int nparts = eta ? nb - 1 : 0;
+  const size_t data_bytes = fcap * size_t(nb - 1) + sizeof(double) * size_t(kcap) * size_t(nparts) +
+                            (idx ? 16 * size_t(nT_cap) : 0);
+  char* data = nullptr;
+  if (const int rc = sweep_scratch(lo, sync_bytes, data_bytes, st, &data)) return rc;
+  // the take counter numbers launches by items per launch, the refine's arrival counter by
+  // the last block's tiles: another shape (or the jump sweep on this region) starts afresh
+  const uint64_t sig = uint64_t(items) * 1000003u ^ (uint64_t(0x5a) << 56) ^
+                       (uint64_t(m) << 48) ^ (uint64_t(W) << 40) ^ (uint64_t(nsteps) << 32) ^
+                       uint64_t(nT);
+  if (lo->sweep_items != items || lo->sweep_sig != sig) {
+    HIP_TRY(hipMemsetAsync(lo->d_sweep, 0, sync_bytes, st));
+    lo->sweep_items = items;
+    lo->sweep_sig = sig;
+  }
+  double* fld = reinterpret_cast<double*>(data);
+  PFlowBufs b{};
+  b.W[0] = w;
+  for (int k = 1; k < nb; ++k) b.W[k] = fld + field_hi * (k - 1);
+  b.W[nb] = w;
+  double* rest = fld + field_hi * (nb - 1);
+  b.part = nparts ? rest : nullptr;
+  b.sync = static_cast<uint32_t*>(lo->d_sweep);
+  b.am_idx = idx;
+  b.am_val = value;
+  b.am_nf = nonfinite;
+  b.am_pv = idx ? rest + lo->ktot * nparts : nullptr;
+  b.am_pi = idx ? reinterpret_cast<int64_t*>(b.am_pv + nT) : nullptr;
+  int rc = DG_OK;
+  switch (lo->NP) {
+#define DG_ADJPF_CASE(NPLV)                                                                  \
+    case NPLV: {                                                                             \
+      PrEO<NPLV> pr;                                                                         \
+      if (!make_prolong_eo<NPLV>(P, &pr))                                                    \
+        return fail(DG_ERR_ARG, "P does not commute with the node reversal (symmetric nodes)"); \
+      if (W == 2 && m == 8)                                                                  \
+        rc = launch_adjp_flow<NPLV, 2, 8>(lo, hi, pr, b, snapshots, eta, mode, tn, dt, nsteps, \
+                                          term, st);                                         \
+      else if (W == 2)                                                                       \
+        rc = launch_adjp_flow<NPLV, 2, 4>(lo, hi, pr, b, snapshots, eta, mode, tn, dt, nsteps, \
+                                          term, st);                                         \
+      else                                                                                   \
+        rc = launch_adjp_flow<NPLV, 1, 4>(lo, hi, pr, b, snapshots, eta, mode, tn, dt, nsteps, \
+                                          term, st);                                         \
+    } break;
+    DG_ADJPF_CASE(2) DG_ADJPF_CASE(3) DG_ADJPF_CASE(4) DG_ADJPF_CASE(5)
+    DG_ADJPF_CASE(6) DG_ADJPF_CASE(7) DG_ADJPF_CASE(8)
+#undef DG_ADJPF_CASE
+    default: return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+  }
+  return rc;
+}
+
+int adj_p_impl(dg_plan* lo, dg_plan* hi, const double* P, double* w, const double* snapshots,
+               double t0, double dt, int nsteps, double* eta, int flags, int64_t* idx,
+               double* value, int64_t* nonfinite, void* stream) {
+  if (!lo || !hi || !P || !w || !snapshots) return fail(DG_ERR_ARG, "null argument");
+  if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
+  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS | DG_ADJ_P_TERMINAL_PROLONG))
+    return fail(DG_ERR_ARG, "unknown flags");
+  bool term = (flags & DG_ADJ_P_TERMINAL_PROLONG) != 0;
+  if (int rc = check_pair(lo, hi)) return rc;
+  if (lo->NP > 8) return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (eta != nullptr && nsteps == 0 && (flags & DG_ADJ_ETA_ASSIGN))
+    HIP_TRY(hipMemsetAsync(eta, 0, sizeof(double) * lo->ktot, st));
+  const int64_t field_lo = lo->ktot * lo->NP, field_hi = hi->ktot * hi->NP;
+  if (term && (nsteps == 0 || p_horner() == 0)) {
+    // the round-3 kernel (and an empty sweep) take the terminal weight from w: form it first
+    if (const int rc = dg_prolong(lo, hi, P, snapshots + int64_t(nsteps) * field_lo, w, stream))
+      return rc;
+    term = false;
+  }
+  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt, as the forward sweep
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  if (p_flow_shape(lo, nsteps)) {
+    const int mode = eta ? (kEtaOn | ((flags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
+                            ((flags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
+                         : 0;
+    return adjp_flow(lo, hi, P, w, snapshots, tn.data(), dt, nsteps, eta, mode, term, idx, value,
+                     nonfinite, st);
+  }
+  if (nsteps > 0) {
+    int launches = 0;
+    for (int n = nsteps; n > 0; n -= chunk_p(lo, n)) ++launches;
+    int l = 0;
+    const double* in = w;
+    for (int n = nsteps; n > 0; ++l) {  // this launch covers steps n-m .. n-1
+      const int m = chunk_p(lo, n);
+      const int n0 = n - m;
+      double* out = (l == launches - 1 && launches > 1)
+                        ? w : ((l % 2 == 0) ? hi->d_scratch : hi->d_scratch2);
+      const int em = ((l == 0 && (flags & DG_ADJ_ETA_ASSIGN)) ? kEtaAssign : 0) |
+                     ((n0 == 0 && (flags & DG_ADJ_ETA_ABS)) ? kEtaAbs : 0);
+      const double* snap = snapshots + int64_t(n0) * field_lo;
+      int rc = DG_OK;
+      switch (lo->NP) {
+#define DG_ADJP_CASE(NPLV)                                                                  \
+        case NPLV: {                                                                        \
+          PrEO<NPLV> pr;                                                                    \
+          if (!make_prolong_eo<NPLV>(P, &pr))                                               \
+            return fail(DG_ERR_ARG, "P does not commute with the node reversal (symmetric nodes)"); \
+          rc = launch_adj_p_t<NPLV>(lo, hi, pr, m, in, out, snap, eta, em, &tn[n0], dt, st,  \
+                                    term && l == 0);                                        \
+        } break;
+        DG_ADJP_CASE(2) DG_ADJP_CASE(3) DG_ADJP_CASE(4) DG_ADJP_CASE(5)
+        DG_ADJP_CASE(6) DG_ADJP_CASE(7) DG_ADJP_CASE(8)
+#undef DG_ADJP_CASE
+        default: return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+      }
+      if (rc) return rc;
+      in = out;
+      n = n0;
+    }
+    if (in != w)  // a one-launch sweep went through scratch
+      HIP_TRY(hipMemcpyAsync(w, in, sizeof(double) * field_hi, hipMemcpyDeviceToDevice, st));
+  }
+  return idx ? dg_argmax_ex(lo, eta, lo->ktot, 1, idx, value, nonfinite, stream) : DG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -596,60 +981,22 @@ int dg_prolong(const dg_plan* lo, const dg_plan* hi, const double* P, const doub
 
 int dg_lserk4_adj_p(dg_plan* lo, dg_plan* hi, const double* P, double* w, const double* snapshots,
                     double t0, double dt, int nsteps, double* eta, int flags, void* stream) {
-  if (!lo || !hi || !P || !w || !snapshots) return fail(DG_ERR_ARG, "null argument");
-  if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
-  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS | DG_ADJ_P_TERMINAL_PROLONG))
-    return fail(DG_ERR_ARG, "unknown flags");
-  bool term = (flags & DG_ADJ_P_TERMINAL_PROLONG) != 0;
-  if (int rc = check_pair(lo, hi)) return rc;
-  if (lo->NP > 8) return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (eta != nullptr && nsteps == 0 && (flags & DG_ADJ_ETA_ASSIGN))
-    HIP_TRY(hipMemsetAsync(eta, 0, sizeof(double) * lo->ktot, st));
-  const int64_t field_lo = lo->ktot * lo->NP, field_hi = hi->ktot * hi->NP;
-  if (term && (nsteps == 0 || p_horner() == 0)) {
-    // the round-3 kernel (and an empty sweep) take the terminal weight from w: form it first
-    if (const int rc = dg_prolong(lo, hi, P, snapshots + int64_t(nsteps) * field_lo, w, stream))
-      return rc;
-    term = false;
-  }
-  if (nsteps == 0) return DG_OK;
-  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt, as the forward sweep
-  tn[0] = t0;
-  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
-  int launches = 0;
-  for (int n = nsteps; n > 0; n -= chunk_p(lo, n)) ++launches;
-  int l = 0;
-  const double* in = w;
-  for (int n = nsteps; n > 0; ++l) {  // this launch covers steps n-m .. n-1
-    const int m = chunk_p(lo, n);
-    const int n0 = n - m;
-    double* out = (l == launches - 1 && launches > 1)
-                      ? w : ((l % 2 == 0) ? hi->d_scratch : hi->d_scratch2);
-    const int em = ((l == 0 && (flags & DG_ADJ_ETA_ASSIGN)) ? kEtaAssign : 0) |
-                   ((n0 == 0 && (flags & DG_ADJ_ETA_ABS)) ? kEtaAbs : 0);
-    const double* snap = snapshots + int64_t(n0) * field_lo;
-    int rc = DG_OK;
-    switch (lo->NP) {
-#define DG_ADJP_CASE(NPLV)                                                                  \
-      case NPLV: {                                                                          \
-        PrEO<NPLV> pr;                                                                      \
-        if (!make_prolong_eo<NPLV>(P, &pr))                                                 \
-          return fail(DG_ERR_ARG, "P does not commute with the node reversal (symmetric nodes)"); \
-        rc = launch_adj_p_t<NPLV>(lo, hi, pr, m, in, out, snap, eta, em, &tn[n0], dt, st,    \
-                                  term && l == 0);                                          \
-      } break;
-      DG_ADJP_CASE(2) DG_ADJP_CASE(3) DG_ADJP_CASE(4) DG_ADJP_CASE(5)
-      DG_ADJP_CASE(6) DG_ADJP_CASE(7) DG_ADJP_CASE(8)
-#undef DG_ADJP_CASE
-      default: return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
-    }
-    if (rc) return rc;
-    in = out;
-    n = n0;
-  }
-  if (in != w)  // a one-launch sweep went through scratch
-    HIP_TRY(hipMemcpyAsync(w, in, sizeof(double) * field_hi, hipMemcpyDeviceToDevice, st));
+  return adj_p_impl(lo, hi, P, w, snapshots, t0, dt, nsteps, eta, flags, nullptr, nullptr,
+                    nullptr, stream);
+}
+
+int dg_lserk4_adj_p_refine(dg_plan* lo, dg_plan* hi, const double* P, double* w,
+                           const double* snapshots, double t0, double dt, int nsteps,
+                           double* eta, int flags, int64_t* idx, double* value,
+                           int64_t* nonfinite_count, void* stream) {
+  if (!idx || !eta) return fail(DG_ERR_ARG, "null argument (the refine decision needs eta)");
+  return adj_p_impl(lo, hi, P, w, snapshots, t0, dt, nsteps, eta, flags, idx, value,
+                    nonfinite_count, stream);
+}
+
+int dg_plan_query_p_flow(const dg_plan* lo, int nsteps, int* out) {
+  if (!lo || !out) return fail(DG_ERR_ARG, "null argument");
+  *out = p_flow_shape(lo, nsteps) ? 1 : 0;
   return DG_OK;
 }
 

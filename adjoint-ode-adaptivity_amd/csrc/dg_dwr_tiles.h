@@ -105,6 +105,98 @@ template <class T> struct KaSrc {
   }
 };
 
+// A workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup release fence
+// as well, and with a direct-to-LDS load in flight the compiler drains vmcnt(0) before it;
+// between the levels nothing but LDS is exchanged, so the loads stay in flight across these.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// tile_issue's interior load straight into the LDS image (global_load_lds_dwordx4: the lanes
+// of a wave write 64 consecutive 16-byte slots from M0, the wave's base): no registers held
+// while the loads are in flight.  Interior tiles only (every 16-byte slot in range).  The
+// image is complete after `s_waitcnt vmcnt(0)` and a barrier.  Returns the image offset.
+template <int NP, int W>
+__device__ __forceinline__ int tile_issue_lds(const double* __restrict__ g, int64_t e0,
+                                              double* __restrict__ lds) {
+  using G = TileGeo<NP, W>;
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) void glb_void;
+  const int64_t d0 = e0 * NP;
+  const int64_t base = d0 & ~int64_t(1);
+  const int off = int(d0 - base);
+  const int nvec = (G::T * NP + off + 1) >> 1;
+  const double* gb = g + base;
+  const int wb = int(threadIdx.x) & ~63;
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = threadIdx.x + q * G::LB;
+    if (v < nvec)
+      __builtin_amdgcn_global_load_lds((glb_void*)(gb + 2 * v), (lds_void*)(lds + 2 * (q * G::LB + wb)),
+                                       16, 0, 0);
+  }
+  return off;
+}
+
+// tile_issue with sc1 loads (dg_rec_tiles.h tile_load's WT policy): the input of a work item
+// of a dataflow launch, written write-through by an earlier item of the same launch.
+template <int NP, int W, bool EDGE>
+__device__ __forceinline__ void tile_issue_wt(const double* __restrict__ g, int64_t e0,
+                                              int64_t nd, TileRegs<NP, W>& r) {
+  using G = TileGeo<NP, W>;
+  const int64_t d0 = e0 * NP;
+  const int64_t base = d0 & ~int64_t(1);
+  r.off = int(d0 - base);
+  const int nvec = (G::T * NP + r.off + 1) >> 1;
+  const int64_t bc = base > 0 ? base : 0;  // (base < 0 only in edge tiles: those lanes load nothing)
+  const __amdgpu_buffer_rsrc_t rs = dgr::wt_rsrc(g + bc);
+#pragma unroll
+  for (int q = 0; q < G::kVec; ++q) {
+    const int v = threadIdx.x + q * G::LB;
+    const int64_t gd = base + 2 * int64_t(v);
+    double2 val = make_double2(0.0, 0.0);
+    if (v < nvec) {
+      if (!EDGE || (gd >= 0 && gd + 1 < nd)) {
+        val = dgr::wt_ld16(rs, uint32_t(gd - bc) * 8u);
+      } else {
+        if (gd >= 0 && gd < nd) val.x = dgr::wt_ld8(rs, uint32_t(gd - bc) * 8u);
+        if (gd + 1 >= 0 && gd + 1 < nd) val.y = dgr::wt_ld8(rs, uint32_t(gd + 1 - bc) * 8u);
+      }
+    }
+    r.v[q] = val;
+  }
+}
+
+// One element's indicator in a dataflow launch (rp_adj_tile's WT branch): a block other than
+// the last writes its partial sum to its own row; the last adds the caller's eta (unless
+// assigning) and the earlier blocks' rows in launch order, then its own -- the additions of
+// the launch-per-block chain, bit for bit -- and keeps the lane's (|eta|, element) winner for
+// the fused refine decision.  ec: the tile's first output element (wave-uniform).
+__device__ __forceinline__ void eta_sink_put(dgr::EtaSink& es, int64_t ec, int64_t e,
+                                             double acc) {
+  const uint32_t o = uint32_t(e - ec) * 8u;
+  if (es.part_out) {
+    dgr::wt_st8(dgr::wt_rsrc(es.part_out + ec), o, acc);
+    return;
+  }
+  double v;
+  if (es.nparts > 0) {
+    v = dgr::wt_ld8(dgr::wt_rsrc(es.part_in + ec), o);
+    if (!(es.mode & kEtaAssign)) v = es.eta[e] + v;
+    for (int q = 1; q < es.nparts; ++q)
+      v = v + dgr::wt_ld8(dgr::wt_rsrc(es.part_in + q * es.part_ld + ec), o);
+    v = v + acc;
+  } else {
+    v = (es.mode & kEtaAssign) ? acc : es.eta[e] + acc;
+  }
+  if (es.mode & kEtaAbs) v = fabs(v);
+  dgr::wt_st8(dgr::wt_rsrc(es.eta + ec), o, v);
+  if (es.argmax && dgr::am_better(fabs(v), e, es.bv, es.bi)) {
+    es.bv = fabs(v);
+    es.bi = e;
+  }
+}
+
 template <int NPL, int W> struct PHGeo {
   static constexpr int NPH = NPL + 1;
   static constexpr int LB = kBlock * W, T = LB;
@@ -117,19 +209,31 @@ template <int NPL, int W> struct PHGeo {
 // One tile of a Horner-form estimate launch.  snap = u^{n0}; reads u^{n0} .. u^{n0+MS}.
 // `ka`: the argument block in the kernarg segment (operator and prolongation reads); `kbnd`:
 // its bnd array there (the edge tiles' lane-indexed reads).
-template <int NPL, bool UNI, int W, int MS, bool EDGE>
+// GL: interior tiles load the next snapshot straight into LDS (tile_issue_lds).  WT: a work
+// item of the one-launch sweep (k_adjp_flow): w is loaded sc1 and stored write-through, and
+// the indicator goes to `es` (this block's partial row, or the final combine in the last
+// block), as the jump sweep's rp_adj_tile does.  A: the argument struct (op, pr, sc, beta,
+// ktot, stride, K, has_eta).  term: the terminal weight is P u^{n0+MS} (win is not read).
+// wait_inputs: called by all threads once the snapshot loads are issued, before w is loaded
+// (a dataflow item's poll of its producers and the barrier after it).
+struct NoWait {
+  __device__ void operator()() const {}
+};
+
+template <int NPL, bool UNI, int W, int MS, bool EDGE, bool GL = false, bool WT = false,
+          class A = AdjPHArgs<NPL, MS>, class WaitF = NoWait>
 __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t tile,
                                            const double* __restrict__ win,
                                            double* __restrict__ wout,
                                            const double* __restrict__ snap,
                                            double* __restrict__ eta,
                                            const double* __restrict__ scale,
-                                           const AdjPHArgs<NPL, MS>& args,
-                                           const DG_KAS AdjPHArgs<NPL, MS>* ka,
-                                           const double* kbnd) {
+                                           const A& args, const DG_KAS A* ka,
+                                           const double* kbnd, bool term,
+                                           dgr::EtaSink* es = nullptr,
+                                           const WaitF& wait_inputs = WaitF()) {
   constexpr int NPH = NPL + 1;
   using G = PHGeo<NPL, W>;
-  using A = AdjPHArgs<NPL, MS>;
   constexpr int T = G::T, LB = G::LB;
   // the reverse cone is 5 elements per step; the forward recompute of a step needs 5 more
   // around the output elements, which the halo of the steps still to come covers
@@ -148,10 +252,15 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
 
   TileRegs<NPH, W> pw;
   TileRegs<NPL, W> pa, pb;
-  const bool term = args.term != 0;
-  if (!term) tile_issue<NPH, W, EDGE>(win, e0, ndh, pw);
+  // the snapshots (an earlier launch's) are loaded while a dataflow item waits for its
+  // producers (wait_inputs), then w
   tile_issue<NPL, W, EDGE>(snap + MS * args.stride, e0, ndl, pa);
   tile_issue<NPL, W, EDGE>(snap + (MS - 1) * args.stride, e0, ndl, pb);
+  wait_inputs();
+  if (!term) {
+    if constexpr (WT) tile_issue_wt<NPH, W, EDGE>(win, e0, ndh, pw);
+    else tile_issue<NPH, W, EDGE>(win, e0, ndh, pw);
+  }
   if (!term) tile_commit<NPH, W>(pw, lds);
   if constexpr (EDGE) {
     if (lane <= MS * 5) lds[CB + lane] = kbnd[lane];  // lane-indexed: from the kernarg segment
@@ -291,8 +400,16 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
     for (int k = 0; k < NO; ++k) no[k] = vo[k];
     // the next snapshot's loads, in flight behind the reverse levels (issued here rather than
     // at the step start: the forward levels hold the most values, and 12 more VGPRs there
-    // would cost a workgroup per CU)
-    if (st > 0) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
+    // would cost a workgroup per CU).  GL: interior tiles load straight into the image (its
+    // readers, the prolongation at the step start, are 5 barriers behind) and edge tiles load
+    // at the step end, so no prefetch registers are held.
+    constexpr bool kGL = GL && !EDGE;
+    int offn = 0;
+    if constexpr (kGL) {
+      if (st > 0) offn = tile_issue_lds<NPL, W>(snap + (st - 1) * args.stride, e0, lds);
+    } else if constexpr (!GL) {
+      if (st > 0) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
+    }
 
     // ---- w^n = S_{N+1}^T w^{n+1} by Horner (rp_adj_tile's level arithmetic at order N+1) ----
 #pragma unroll
@@ -362,7 +479,8 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
 #pragma unroll
         for (int k = 0; k < NE; ++k) pin(ae[k]);
       }
-      __syncthreads();
+      if constexpr (GL) lds_barrier();
+      else __syncthreads();
       // nothing arrives at a trajectory's first element from the left (its uL is the
       // inflow); its last element's uR is its own u_N (du1 = 0)
       const double gl = lds[EDGE && E.first ? CB + MS * 5 : f1 + lane];
@@ -385,13 +503,23 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
     // the image's readers (the prolongation at the step start) are 10 level barriers behind;
     // the next step's prolongation reads what every wave commits here
     if (st > 0) {
-      tile_commit<NPL, W>(pa, lds);
-      off = pa.off;
+      if constexpr (kGL) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        off = offn;
+      } else {
+        if constexpr (GL) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
+        tile_commit<NPL, W>(pa, lds);
+        off = pa.off;
+      }
       __syncthreads();
     }
   }
 
-  if (args.has_eta && E.valid) eta_update(eta, E.e, eacc, args.has_eta);
+  if constexpr (WT) {
+    if (args.has_eta && E.valid) eta_sink_put(*es, tile * TE, E.e, eacc);
+  } else {
+    if (args.has_eta && E.valid) eta_update(eta, E.e, eacc, args.has_eta);
+  }
   {
     const double(*pwe)[NE] = &we;
     const double(*pwo)[NO] = &wo;
@@ -401,9 +529,13 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
   const int64_t o0 = tile * TE * NPH;
   if constexpr (EDGE) {
     const int64_t rem = ndh - o0;
-    store_run<LB>(wout, o0, rem < int64_t(TE) * NPH ? rem : int64_t(TE) * NPH, lds);
+    if constexpr (WT)
+      dgr::store_run_wt<LB>(wout, o0, rem < int64_t(TE) * NPH ? rem : int64_t(TE) * NPH, lds);
+    else
+      store_run<LB>(wout, o0, rem < int64_t(TE) * NPH ? rem : int64_t(TE) * NPH, lds);
   } else {
-    store_full<TE * NPH, LB>(wout, o0, lds);
+    if constexpr (WT) dgr::store_full_wt<TE * NPH, LB>(wout, o0, lds);
+    else store_full<TE * NPH, LB>(wout, o0, lds);
   }
 }
 

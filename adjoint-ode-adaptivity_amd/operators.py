@@ -535,10 +535,14 @@ class DWREstimate:
     self._P, self._P_ptr = _lib.dbl_array(self.P)
     self.tune(tile_width, steps_per_launch)
 
-  def tune(self, tile_width=None, steps_per_launch=None):
+  def tune(self, tile_width=None, steps_per_launch=None, flow=None):
     """Tiles of 256*``tile_width`` elements (1, 2) and ``steps_per_launch`` (1, 2, 4; 8 on
-    512-element tiles) reverse steps per launch of dg_lserk4_adj_p."""
+    512-element tiles) reverse steps per launch of dg_lserk4_adj_p; ``flow`` (0 / 1): one
+    launch per block, or the whole estimate as one dataflow launch where the steps split
+    into 2 or more blocks of 4 (or 8 on 512-element tiles) steps (bit-identical)."""
     lib, plan = self.lo._lib, self.lo._plan
+    if flow is not None:
+      _lib.check(lib.dg_plan_tune(plan, _lib.DG_TUNE_P_FLOW, int(flow)), "dg_plan_tune")
     if tile_width is not None:
       _lib.check(lib.dg_plan_tune(plan, _lib.DG_TUNE_P_TILE_WIDTH, int(tile_width)), "dg_plan_tune")
     if steps_per_launch is not None:
@@ -548,6 +552,13 @@ class DWREstimate:
     _lib.check(lib.dg_plan_query_p(plan, q), "dg_plan_query_p")
     self.tile_width, self.steps_per_launch = int(q[0]), int(q[1])
     return self
+
+  def query_flow(self, nsteps):
+    """True if ``estimate`` over ``nsteps`` steps runs as one dataflow launch."""
+    out = ctypes.c_int32()
+    _lib.check(self.lo._lib.dg_plan_query_p_flow(self.lo._plan, int(nsteps), ctypes.byref(out)),
+               "dg_plan_query_p_flow")
+    return bool(out.value)
 
   def new_field(self, count=None):
     return self.hi.new_field(count)
@@ -580,6 +591,32 @@ class DWREstimate:
         float(t0), float(dt), int(nsteps), eta_p, int(flags), _stream(self.lo.device))
     _lib.check(rc, "dg_lserk4_adj_p")
     return w, eta
+
+  def estimate_refine(self, w, snapshots, t0, dt, nsteps, eta, idx, value=None, nonfinite=None,
+                      eta_assign=True, eta_abs=True, terminal_prolong=False):
+    """``estimate`` + the refine decision ``argmax_ex(eta, use_abs=True)`` in one call
+    (dg_lserk4_adj_p_refine): in the dataflow launch the last block's tiles reduce the argmax
+    themselves.  ``idx`` / ``nonfinite`` (CUDA int64, 1) and ``value`` (CUDA float64, 1) as
+    for ``argmax_ex``."""
+    def p1(t, dtype, name):
+      if t is None:
+        return None
+      if isinstance(t, int):  # a device address (host_alias of pinned host memory)
+        return ctypes.c_void_p(t)
+      if not t.is_cuda or t.dtype != dtype or t.numel() < 1:
+        raise TypeError(f"{name} must be a CUDA {dtype} tensor or a device address")
+      return ctypes.c_void_p(t.data_ptr())
+    flags = ((_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) |
+             (_lib.DG_ADJ_ETA_ABS if eta_abs else 0) |
+             (_lib.DG_ADJ_P_TERMINAL_PROLONG if terminal_prolong else 0))
+    rc = self.lo._lib.dg_lserk4_adj_p_refine(
+        self.lo._plan, self.hi._plan, self._P_ptr, self.hi._field(w, "w"),
+        self.lo._field(snapshots, "snapshots", (nsteps + 1) * self.lo.field_numel),
+        float(t0), float(dt), int(nsteps), self.lo._field(eta, "eta", self.lo.ktot), int(flags),
+        p1(idx, torch.int64, "idx"), p1(value, torch.float64, "value"),
+        p1(nonfinite, torch.int64, "nonfinite"), _stream(self.lo.device))
+    _lib.check(rc, "dg_lserk4_adj_p_refine")
+    return idx
 
   def close(self):
     self.hi.close()

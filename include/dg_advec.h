@@ -143,12 +143,17 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             (bit-identical to the record sweeps' stage loop), 1 the Horner-form
  *                             step on pair tiles (512 * tile width elements, steps per launch as
  *                             DG_TUNE_STEPS_PER_LAUNCH; equal to the stage loop to rounding)
+ *   DG_TUNE_P_FLOW            dg_lserk4_adj_p: 1 runs the estimate as ONE dataflow launch (the
+ *                             blocks' tiles are work items; the jump sweep's hand-offs and
+ *                             watchdog) when nsteps splits into 2 .. 40/steps-per-launch blocks
+ *                             of the plan's steps per launch; 0 one launch per block.
+ *                             Bit-identical results
  *   DG_TUNE_SWEEP_SPIN_LIMIT  diagnostics/tests: polls a dataflow work item makes before it
  *                             gives up waiting for a producer (0: the default, ~2^20; 1 makes
  *                             the watchdog fire on any multi-block sweep)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
  * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
- * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE, DG_SNAP_PAIRS. */
+ * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE, DG_SNAP_PAIRS, DG_P_FLOW. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
@@ -156,7 +161,7 @@ enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER =
        DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12,
        DG_TUNE_SWEEP_SPIN_LIMIT = 13, DG_TUNE_SWEEP_WAVES = 14,
        DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16, DG_TUNE_SWEEP_EXCHANGE = 17,
-       DG_TUNE_SNAP_PAIRS = 18 };
+       DG_TUNE_SNAP_PAIRS = 18, DG_TUNE_P_FLOW = 19 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
@@ -361,12 +366,29 @@ int dg_plan_sweep_trace(dg_plan* plan, uint64_t* trace);
  *   snapshots: the (nsteps+1) order-N states dg_lserk4_fwd wrote (snapshots[n] = u^n).
  *   eta (nullable, batch*K) and flags as dg_lserk4_adj_ex (DG_ADJ_ETA_ASSIGN / _ABS), plus
  *   DG_ADJ_P_TERMINAL_PROLONG (w on entry := P u^nsteps, formed in the kernel).
- * Scratch: the hi plan's.  Neither plan may be used concurrently. */
+ * Scratch: the hi plan's; the dataflow form (DG_TUNE_P_FLOW) the lo plan's dataflow region
+ * (as dg_lserk4_sweep_rec; its watchdog flag is the lo plan's, dg_sweep_status).  Neither plan
+ * may be used concurrently. */
 int dg_prolong(const dg_plan* lo, const dg_plan* hi, const double* P, const double* u,
                double* u_hi, void* stream);
 int dg_lserk4_adj_p(dg_plan* lo, dg_plan* hi, const double* P, double* w,
                     const double* snapshots, double t0, double dt, int nsteps, double* eta,
                     int flags, void* stream);
+
+/* dg_lserk4_adj_p followed by the refine decision dg_argmax_ex(lo, eta, ktot, use_abs = 1,
+ * idx, value, nonfinite_count), as dg_lserk4_sweep_refine does for the jump indicator: fused
+ * into the launch (the last block's tiles reduce their winners) when the estimate runs as one
+ * dataflow launch (DG_TUNE_P_FLOW), else a separate reduction.  eta and idx are required.
+ * Replaces python/Main_finite_difference.py:336-341 (np.argmax of the indicator). */
+int dg_lserk4_adj_p_refine(dg_plan* lo, dg_plan* hi, const double* P, double* w,
+                           const double* snapshots, double t0, double dt, int nsteps,
+                           double* eta, int flags, int64_t* idx, double* value,
+                           int64_t* nonfinite_count, void* stream);
+
+/* *out = 1 if dg_lserk4_adj_p over nsteps steps runs as one dataflow launch on the lo plan's
+ * current settings (DG_TUNE_P_FLOW, steps per launch 4, or 8 on 512-element tiles, 2..40/MS
+ * blocks), else 0. */
+int dg_plan_query_p_flow(const dg_plan* lo, int nsteps, int* out);
 
 /* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */
