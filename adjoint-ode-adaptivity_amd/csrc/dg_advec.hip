@@ -1342,11 +1342,13 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     p->rec_tile_width = 1;
     p->rec_tile_width_fwd = 2;
   }
-  // The p-enriched estimate (dg_lserk4_adj_p, Horner form since round 5) on 256-element tiles:
-  // 88-90 us per 4-step launch at N = 4, K = 2^20 against 98-100 on 512-element tiles (the
-  // body's 94 VGPRs leave 5 waves per SIMD, which only 4-wave workgroups fill;
-  // profiles/r05/p1, p2)
-  p->p_tile_width = 1;
+  // The p-enriched estimate (dg_lserk4_adj_p, Horner form since round 5) as ONE dataflow
+  // launch (k_adjp_flow) on 512-element tiles with 4-step blocks: 410 us per 20-step estimate
+  // at N = 4, K = 2^20 against 437 for the launch chain of direct-to-LDS 256-element tiles and
+  // 443 for the chain with register prefetch (profiles/r05/p13; the chain drains each launch:
+  // 4,855 tiles are 3.16 rounds of the 1,536 resident workgroups).
+  p->p_tile_width = 2;
+  p->p_flow = 1;
   {
     if (const char* v = std::getenv("DG_TILE_WIDTH")) {
       const int k = std::atoi(v);

@@ -457,7 +457,7 @@ struct dg_plan {
   int p_tile_width = 2;
   int p_msteps = 4;
   // 1: the estimate runs as ONE dataflow launch (k_adjp_flow) when its steps split into >= 2
-  // blocks of p_msteps; 0: one launch per block
+  // blocks of p_msteps; 0: one launch per block (dg_plan_create sets 1)
   int p_flow = 0;
   // the dataflow sweep (dg_lserk4_sweep_rec, dg_sweep.hip): its scratch (sync words, block
   // states, indicator partials; grown on demand) and the switch (1: one dataflow launch where

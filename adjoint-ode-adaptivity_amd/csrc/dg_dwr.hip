@@ -536,8 +536,9 @@ template <int NPL, int MS> struct AdjPFArgs {
   const double* scale;
   uint32_t* sync;                        // kSync* words, then one flag per item
   uint32_t* err_host;
-  uint64_t* trace;                       // nullable: per item {dequeued, producers done,
-                                         // published, XCC id << 32 | workgroup id}
+  uint64_t* trace;                       // nullable: 8 words per item {started, dequeued,
+                                         // producers done, body done, published, XCC id << 32
+                                         // | workgroup id, 0, 0} (wall clock, 100 MHz)
   int64_t* am_idx;                       // nullable: the fused refine decision
   double* am_val;
   int64_t* am_nf;
@@ -569,6 +570,7 @@ void k_adjp_flow(AdjPFArgs<NPL, MS> a) {
   uint32_t* flags = sync + dgr::kSyncFlags;
   const int tid = threadIdx.x;
   const int nT = a.nT, nb = a.nb;
+  const uint64_t t_start = a.trace ? uint64_t(wall_clock64()) : 0;
   if (tid == 0) {
     uint32_t it, ep;
     dgr::flow_take(sync, int64_t(nb) * nT, &it, &ep);
@@ -646,6 +648,7 @@ void k_adjp_flow(AdjPFArgs<NPL, MS> a) {
     }
   }
   // publish: every wave's write-through stores have completed, then one flag store
+  const uint64_t t_body = a.trace ? uint64_t(wall_clock64()) : 0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) dgr::st_agent(flags + item, epoch);
@@ -655,11 +658,13 @@ void k_adjp_flow(AdjPFArgs<NPL, MS> a) {
   if (a.trace && tid == 0) {
     uint32_t xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uint64_t* tr = a.trace + 4 * item;
-    tr[0] = t_deq;
-    tr[1] = t_ready;
-    tr[2] = uint64_t(wall_clock64());
-    tr[3] = (uint64_t(xcc) << 32) | blockIdx.x;
+    uint64_t* tr = a.trace + 8 * item;
+    tr[0] = t_start;
+    tr[1] = t_deq;
+    tr[2] = t_ready;
+    tr[3] = t_body;
+    tr[4] = uint64_t(wall_clock64());
+    tr[5] = (uint64_t(xcc) << 32) | blockIdx.x;
   }
 }
 
@@ -731,16 +736,18 @@ int launch_adjp_flow(dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const 
   return DG_OK;
 }
 
-// DG_P_HORNER (read once, A/B runs): 0 round 3's stage loop (k_adj_p), 1 (default) Horner
-// (k_adj_ph), 2 Horner pipelined (k_adj_pq: the forward recompute of step n-1 beside the
-// reverse step n, half the barriers; 125 VGPRs, 4 waves per SIMD: measured 2-5 % slower than
-// k_adj_ph, profiles/r05/p3), 3 Horner with the snapshot tiles loaded straight into LDS
-// (k_adj_ph<..., GL = true>: no prefetch registers)
+// DG_P_HORNER (read once, A/B runs): 0 round 3's stage loop (k_adj_p), 1 Horner (k_adj_ph)
+// with the next snapshot tile prefetched into registers (94 VGPRs at Np = 5: 5 waves per
+// SIMD), 2 Horner pipelined (k_adj_pq: the forward recompute of step n-1 beside the reverse
+// step n, half the barriers; 125 VGPRs, 4 waves per SIMD: measured 2-5 % slower than
+// k_adj_ph, profiles/r05/p3), 3 (default) Horner with the snapshot tiles loaded straight into
+// LDS (k_adj_ph<..., GL = true>: 80 VGPRs, 6 waves per SIMD; 1-2 % faster than 1,
+// profiles/r05/p5, p13).  The dataflow launch (k_adjp_flow) always loads into LDS.
 inline int p_horner() {
   static const int v = [] {
     const char* e = std::getenv("DG_P_HORNER");
-    const int k = e ? std::atoi(e) : 1;
-    return (k == 0 || k == 2 || k == 3) ? k : 1;
+    const int k = e ? std::atoi(e) : 3;
+    return (k == 0 || k == 1 || k == 2) ? k : 3;
   }();
   return v;
 }

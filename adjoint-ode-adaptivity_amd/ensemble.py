@@ -164,14 +164,33 @@ class EnsembleSweep:
     """``sweep`` plus the refine decision into ``reducer`` (index, value, non-finite count:
     the DeviceReducer state) in ONE dg_lserk4_sweep_refine call -- for a single trajectory on
     a single rank, whose indicator is the whole mean (Main_width_ref.py:479 with one IC); the
-    dataflow launch reduces the argmax in its last tiles.  ``idx`` / ``value``: other
+    dataflow launch reduces the argmax in its last tiles (the p-estimate: the snapshot forward,
+    then dg_lserk4_adj_p_refine).  ``idx`` / ``value``: other
     destinations for the index and value (e.g. ``operators.host_alias`` addresses of pinned
     host memory: the decision lands on the host with no copy launch)."""
-    if self.record != "jumps" or self.batch != 1:
-      raise ValueError("sweep_refine: one trajectory with the jump record")
+    if self.batch != 1 or (self.record != "jumps" and self.est is None):
+      raise ValueError("sweep_refine: one trajectory with the jump record or the p-estimate")
+    idx = reducer.idx if idx is None else idx
+    value = reducer.value if value is None else value
+    if self.est is not None:
+      # the p-estimate: the snapshot forward, then the estimate with the refine decision
+      # (fused into its dataflow launch where the shape allows, dg_lserk4_adj_p_refine)
+      self.forward()
+      self.estimate_refine(idx, value, reducer.nonfinite)
+      return
     self.op.sweep_refine(self.u0, self.jumps, self.w, 0.0, self.dt, self.nsteps, self.eta,
-                         reducer.idx if idx is None else idx,
-                         reducer.value if value is None else value, reducer.nonfinite)
+                         idx, value, reducer.nonfinite)
+
+  def estimate_refine(self, idx, value, nonfinite):
+    """The p-estimate's adjoint (``run_adjoint``) + the refine decision in one call."""
+    self.est.estimate_refine(self.w, self.snaps, 0.0, self.dt, self.nsteps, self.eta, idx,
+                             value, nonfinite, eta_assign=True, eta_abs=True,
+                             terminal_prolong=True)
+
+  @property
+  def p_dataflow(self):
+    """True when the p-estimate runs as ONE dataflow launch (dg_lserk4_adj_p, DG_TUNE_P_FLOW)."""
+    return self.est is not None and self.est.query_flow(self.nsteps)
 
   def capture(self):
     """Capture the sweep as HIP graphs (replayed by sweep_graph, or forward_graph /

@@ -675,7 +675,11 @@ def main(argv=None):
   # one trajectory on one rank the indicator is the whole mean, so the refine decision is
   # reduced inside the same launch (dg_lserk4_sweep_refine).
   dataflow = sweep.dataflow
-  fused_refine = (dataflow and world == 1 and sweep.batch == 1 and not args.gather_ics
+  # the p-estimate as ONE dataflow launch (dg_lserk4_adj_p, k_adjp_flow) after the snapshot
+  # forward's launches; with one trajectory on one rank its last block reduces the refine
+  # decision too (dg_lserk4_adj_p_refine)
+  pflow = args.indicator == "p" and sweep.p_dataflow
+  fused_refine = ((dataflow or pflow) and world == 1 and sweep.batch == 1 and not args.gather_ics
                   and not args.graph)
   # The refine index (the mesh split's input) and the indicator there go to the host in one
   # async copy into pinned memory, read after the timed region has synced.  (The copy on a
@@ -691,6 +695,20 @@ def main(argv=None):
   def one_step(ev=None):
     if ev:
       ev[0].record(stream)
+    if fused_refine and pflow:
+      sweep.forward()
+      if ev:
+        ev[1].record(stream)
+        ev[3].record(stream)
+      if res_alias is not None:
+        sweep.estimate_refine(res_alias, res_alias + 8, reducer.nonfinite)
+      else:
+        sweep.estimate_refine(reducer.idx, reducer.value, reducer.nonfinite)
+      if ev:
+        ev[2].record(stream)
+      if res_alias is None:
+        copy_result()
+      return
     if fused_refine:
       if res_alias is not None:
         sweep.sweep_refine(reducer, idx=res_alias, value=res_alias + 8)
@@ -770,7 +788,8 @@ def main(argv=None):
     adj_us = [e[0].elapsed_time(e[2]) * 1e3 for e in evs]
   else:
     fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / len(fchunks) for e in evs]
-    adj_us = [e[3].elapsed_time(e[2]) * 1e3 / len(chunks) for e in evs]
+    # the p-estimate's one dataflow launch: its whole time (its blocks are not separate)
+    adj_us = [e[3].elapsed_time(e[2]) * 1e3 / (1 if pflow else len(chunks)) for e in evs]
   prolong_us = [e[1].elapsed_time(e[3]) * 1e3 for e in evs] if pmode else None
   step_ms = [evs[i][0].elapsed_time(evs[i + 1][0] if i + 1 < len(evs) else ev_end)
              for i in range(len(evs))]
@@ -797,8 +816,8 @@ def main(argv=None):
     adj_bytes = float(np.mean([(16.0 * Np + 8.0 * m + 16.0) * ktot for m in chunks]))
   elif pmode:
     fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
-    adj_bytes = float(np.mean([(16.0 * (Np + 1) + 8.0 * (m + 1) * Np + 16.0) * ktot
-                               for m in chunks]))
+    adj_bytes = float((np.sum if pflow else np.mean)(
+        [(16.0 * (Np + 1) + 8.0 * (m + 1) * Np + 16.0) * ktot for m in chunks]))
   else:
     fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
@@ -806,7 +825,7 @@ def main(argv=None):
   pairs = args.record == "jumps" and getattr(sweep.op, "rec_lane_elements", 1) == 2
   kadj, kstep = ("k_adj_rp", "k_step_rp") if pairs else ("k_adj", "k_step")
   if pmode:
-    kadj = "k_adj_p"
+    kadj = "k_adjp_flow" if pflow else "k_adj_p"
   if dataflow:
     kadj = "k_sweep_rp"
   tile_tag = tile_tag_fwd = f"{tw},2 elements/lane" if pairs else f"{tw}"
@@ -856,6 +875,7 @@ def main(argv=None):
       continue
     if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
         and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
+        and bool(tr.get("p_flow")) == pflow and (not pmode or tr.get("tile_width", tw) == tw)
         and tr.get("record", "snapshots") == args.record
         and tr.get("indicator", "jump") == args.indicator
         and same_kernel(tr)):
@@ -889,7 +909,8 @@ def main(argv=None):
   import torch.distributed as dist
   dist_world = dist.get_world_size() if dist.is_initialized() else 1
   idx_ranks = ranks_agree(ref_idx, world, dev, args.backend)
-  upl = Np * ktot * float(np.mean(chunks))  # DOF-updates per launch (sweep average)
+  # DOF-updates per launch (sweep average; the p-estimate's dataflow launch: all its blocks)
+  upl = Np * ktot * (float(np.sum(chunks)) if pflow else float(np.mean(chunks)))
   fupl = Np * ktot * float(np.mean(fchunks))
   horner = args.record == "jumps" and (pairs or dataflow)  # dg_rec_tiles.h's Horner-form steps
   if pmode:
@@ -1003,6 +1024,24 @@ def main(argv=None):
         f["pmc_source"] = os.path.relpath(os.path.join(prof_dir, "sq_summary.json"), ROOT)
     except (OSError, ValueError, KeyError, TypeError):
       pass
+  if pflow:
+    r = out["roofline"]
+    r["kernel"] = (f"k_adjp_flow<{Np - 1}+1,uniform,{256 * tw} elements,{ms} steps per block> "
+                   f"(ONE dataflow launch per estimate: {len(chunks)} blocks of {ms} reverse "
+                   f"steps + DWR{' + refine decision' if fused_refine else ''})")
+    r["note"] = ("p-estimate as one dataflow launch (dg_lserk4_adj_p, DG_TUNE_P_FLOW): the blocks' "
+                 "tiles are the work items; per reverse step the order-(N+1) forward step from "
+                 "the prolonged snapshot and the order-(N+1) reverse step (roofline_fp64); "
+                 "algorithmic bytes = the blocks' sum")
+    out["p_dataflow"] = {"launches_per_estimate": 1, "blocks": chunks,
+                         "refine_in_launch": fused_refine,
+                         "refine_to_host": ("written by the launch into pinned memory "
+                                            "(dg_host_alias)" if res_alias is not None
+                                            else "async copy"),
+                         "work_items": len(chunks) * -(-ktot // (256 * tw - 10 * ms)),
+                         "status": sweep.op.sweep_status()}
+    if out["p_dataflow"]["status"]:
+      raise RuntimeError("a p-estimate work item gave up waiting for a producer")
   if dataflow:
     r = out["roofline"]
     r["kernel"] = (f"k_sweep_rp<{Np},uniform,{T_pair} elements,fwd {'+'.join(map(str, fchunks))},"
@@ -1027,7 +1066,7 @@ def main(argv=None):
     try:
       with open(os.path.join(prof_dir, "sq_summary.json")) as fh:
         sq = json.load(fh)
-      if same_kernel(sq.get("kernel")):
+      if ksig is None or any(str(n).startswith(ksig["name"]) for n in (sq.get("kernel") or [])):
         fl = sq["fp64_flops_issued_per_launch"]
         f["pmc_issued_per_launch"] = fl
         f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS

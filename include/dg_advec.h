@@ -143,7 +143,7 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             (bit-identical to the record sweeps' stage loop), 1 the Horner-form
  *                             step on pair tiles (512 * tile width elements, steps per launch as
  *                             DG_TUNE_STEPS_PER_LAUNCH; equal to the stage loop to rounding)
- *   DG_TUNE_P_FLOW            dg_lserk4_adj_p: 1 runs the estimate as ONE dataflow launch (the
+ *   DG_TUNE_P_FLOW            dg_lserk4_adj_p: 1 (default) runs the estimate as ONE dataflow launch (the
  *                             blocks' tiles are work items; the jump sweep's hand-offs and
  *                             watchdog) when nsteps splits into 2 .. 40/steps-per-launch blocks
  *                             of the plan's steps per launch; 0 one launch per block.

@@ -26,10 +26,10 @@ python3 - "$OUT/bench_under_rocprof.json" > "$OUT/meta.txt" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
 c = d["config"]
-print(c["N"], c["K"], c.get("trajectories_per_gpu", 1), d.get("steps_per_launch", 0), c.get("record", "jumps"), d.get("indicator", "jump"))
+print(c["N"], c["K"], c.get("trajectories_per_gpu", 1), d.get("steps_per_launch", 0), c.get("record", "jumps"), d.get("indicator", "jump"), d.get("tile_width", 1))
 PY
-read N K BATCH SPL REC IND < "$OUT/meta.txt"
-python3 profiles/summarize.py --stats "$STATS" --fetch "$FETCH" --write "$WRITE" --out "$OUT/summary.json" --traffic-json "$OUT/pmc_traffic.json" --N $N --K $K --batch $BATCH --record $REC --steps-per-launch $SPL --indicator $IND > /dev/null || exit 1
+read N K BATCH SPL REC IND TW < "$OUT/meta.txt"
+python3 profiles/summarize.py --stats "$STATS" --fetch "$FETCH" --write "$WRITE" --out "$OUT/summary.json" --traffic-json "$OUT/pmc_traffic.json" --N $N --K $K --batch $BATCH --record $REC --steps-per-launch $SPL --indicator $IND --tile-width $TW > /dev/null || exit 1
 python3 profiles/r04/sq_reduce.py "$OUT" "$KSUB" > /dev/null || exit 1
 # the dataflow kernel's signature (instantiation + occupancy target) the bench matches on
 python3 - "$OUT/bench_under_rocprof.json" "$OUT/pmc_traffic.json" <<'PY'

@@ -1,4 +1,11 @@
+# Per-item timeline of the one-launch p-estimate (probes/pflow_trace.py) at 256- and
+# 512-element tiles, with the chain and the dataflow launch timed alternately; alone, and
+# after the snapshot forward as the bench runs it
 set -o pipefail
-mkdir -p gpurun_out/r05/p11
-timeout -k 10 300 python profiles/r05/probes/pflow_trace.py 1 4 > gpurun_out/r05/p11/trace_w1.json 2> gpurun_out/r05/p11/trace_w1.err || { tail gpurun_out/r05/p11/trace_w1.err; exit 1; }
-cat gpurun_out/r05/p11/trace_w1.json
+o=gpurun_out/r05/p11; mkdir -p $o
+for tw in 1 2; do
+  for f in alone fwd; do
+    timeout -k 10 300 python profiles/r05/probes/pflow_trace.py $tw 4 $f > $o/trace_w${tw}_$f.json 2> $o/trace_w${tw}_$f.err || { tail $o/trace_w${tw}_$f.err; exit 1; }
+  done
+done
+echo all-done

@@ -42,6 +42,7 @@ def main():
   p.add_argument("--batch", type=int, default=1)
   p.add_argument("--record", default="jumps", choices=("jumps", "snapshots"))
   p.add_argument("--indicator", default="jump", choices=("jump", "p"))
+  p.add_argument("--tile-width", type=int, default=None)
   a = p.parse_args()
   out = collections.OrderedDict()
   for r in csv.DictReader(open(a.stats)):
@@ -74,13 +75,19 @@ def main():
       return keys, sum(hbm(k) * out[k]["fetch_dispatches"] for k in keys) / n
 
     adj, adj_b = sweep_mean("k_adj_p" if a.indicator == "p" else "k_adj")
+    p_flow = False
+    if a.indicator == "p":
+      pf, pf_b = sweep_mean("k_adjp_flow")
+      if pf:  # the p-estimate as one dataflow launch
+        adj, adj_b, p_flow = pf, pf_b, True
     fwd, fwd_b = sweep_mean("k_step")
     dataflow = False
     sw, sw_b = sweep_mean("k_sweep_rp")
     if sw:  # the dataflow sweep: one launch per sweep carries both directions' traffic
       adj, adj_b, fwd, fwd_b, dataflow = sw, sw_b, [], None, True
     tr = {"N": a.N, "K": a.K, "batch": a.batch, "steps_per_launch": a.steps_per_launch,
-          "record": a.record, "indicator": a.indicator, "dataflow": dataflow, "source": a.out,
+          "record": a.record, "indicator": a.indicator, "dataflow": dataflow, "p_flow": p_flow,
+          "tile_width": a.tile_width, "source": a.out,
           "adj_kernel": adj, "adj_bytes_per_launch": adj_b,
           "fwd_kernel": fwd, "fwd_bytes_per_launch": fwd_b,
           "note": "FETCH_SIZE x2 (gfx950 16-B/lane half count) + WRITE_SIZE, KiB->bytes; "

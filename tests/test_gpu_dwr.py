@@ -108,6 +108,16 @@ def test_estimate_matches_oracle(pkg, gpu, N):
   check(out)
 
 
+@pytest.mark.parametrize("N,K,nsteps,batch", [(4, 1000, 8, 1), (3, 700, 12, 2), (2, 300, 20, 1)])
+def test_estimate_dataflow_matches_oracle(pkg, gpu, N, K, nsteps, batch):
+  """The default shape runs the estimate as ONE dataflow launch (k_adjp_flow) when the steps
+  split into >= 2 blocks of 4: against the oracle directly (test_gpu_pflow.py: bit for bit
+  against the launch chain)."""
+  out, est = run_case(pkg, gpu, N, K, nsteps, batch=batch, seed=N + 40)
+  assert est.query_flow(nsteps)
+  check(out)
+
+
 @pytest.mark.parametrize("inflow", ["a", "a2", "zero"])
 def test_estimate_inflow_variants(pkg, gpu, inflow):
   out, _ = run_case(pkg, gpu, 4, 777, 5, inflow=inflow, t0=0.013)
@@ -293,7 +303,7 @@ def test_full_size_p_estimate(pkg, gpu):
   1e-10 of max|oracle|, plus the refine index (numpy's argmax of |eta|).  The IC is a sine
   plus per-node noise so the residual is resolved (see test_gpu_full_size.py)."""
   out, est = run_case(pkg, gpu, 4, 1 << 20, 4, seed=21)
-  assert (est.tile_width, est.steps_per_launch) == (1, 4)  # the default launch shape (round 5)
+  assert (est.tile_width, est.steps_per_launch) == (2, 4)  # the default launch shape (round 5)
   check(out)
   eta, eta_ref = out[0][0], out[0][1]
   a = np.sort(np.abs(eta_ref))
