@@ -459,6 +459,9 @@ struct dg_plan {
   // 1: the estimate runs as ONE dataflow launch (k_adjp_flow) when its steps split into >= 2
   // blocks of p_msteps; 0: one launch per block (dg_plan_create sets 1)
   int p_flow = 0;
+  // 1: dg_lserk4_sweep_p runs forward and estimate as ONE dataflow launch (k_psweep) where the
+  // shape allows; 0: the chains (dg_plan_create sets 1)
+  int p_sweep = 0;
   // the dataflow sweep (dg_lserk4_sweep_rec, dg_sweep.hip): its scratch (sync words, block
   // states, indicator partials; grown on demand) and the switch (1: one dataflow launch where
   // the shape allows it, 0: the launch-per-block pair)

@@ -736,6 +736,269 @@ int launch_adjp_flow(dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const 
   return DG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The p-estimate's WHOLE sweep -- the order-N snapshot forward and the estimate -- as ONE
+// dataflow launch (k_psweep, dg_lserk4_sweep_p).  The forward's launches drain like the
+// estimate's did (k_step at 8 steps per launch: 2,428 tiles are 3.16 rounds of the resident
+// workgroups; SQ: 4.1 of 6-7 waves per SIMD resident on average, profiles/r05/p).  Items, in
+// queue order: forward block 0 tiles 0..nT-1 (steps 0..MS-1), forward block 1, ..., then the
+// estimate's blocks as k_adjp_flow.  Forward item (b, k) waits for forward block b-1's tiles
+// k-1..k+1 (its input u^{b MS} is that block's last snapshot); estimate block 0 tile j waits
+// for the last forward block's tiles j-1..j+1 -- whose completion implies every earlier
+// forward block's snapshots around them, the cone growing a tile per block -- and later
+// estimate blocks as k_adjp_flow.  Every snapshot is stored write-through and every load of
+// one (the forward's input, the estimate's tiles, also direct-to-LDS) is sc1, after the poll.
+// Forward and estimate tiles are both 256 * W elements with MS-step blocks (H = 5 MS), so the
+// forward's arithmetic is k_step's at MS steps per launch: bit-identical to dg_lserk4_fwd
+// with that steps-per-launch followed by dg_lserk4_adj_p.
+// ---------------------------------------------------------------------------
+constexpr int kPSMaxSteps = 32;  // 8 blocks of 4: the blocks' constants fit the kernarg segment
+
+template <int NPL, int MS> struct PSweepArgs {
+  static constexpr int kMaxBlocks = kPSMaxSteps / MS;
+  // the estimate's (names as AdjPHArgs: adjph_tile reads them)
+  EOArgs<NPL + 1> op;
+  PrEO<NPL> pr;
+  double sc;
+  double beta[6];
+  double bnd[kMaxBlocks * (MS * 5 + 1)];
+  // the forward's: its operator (order N) and each block's stage inflow values (StepArgs uin)
+  EOArgs<NPL> fop;
+  double fuin[kMaxBlocks * (MS * 5 + 1)];
+  double* snap;                          // u^0 (the caller's) .. u^nsteps, `stride` apart
+  double* W[kMaxBlocks + 1];
+  double* eta;
+  double* part;
+  const double* scale;                   // the estimate's metric (hi plan)
+  const double* fscale;                  // the forward's (lo plan)
+  uint32_t* sync;
+  uint32_t* err_host;
+  uint64_t* trace;                       // nullable: 8 words per item as k_adjp_flow's
+  int64_t* am_idx;
+  double* am_val;
+  int64_t* am_nf;
+  double* am_pv;
+  int64_t* am_pi;
+  int64_t ktot;
+  int64_t stride;
+  int32_t K;
+  int32_t has_eta;
+  int32_t nb;                            // blocks per direction
+  int32_t nT;                            // tiles per block (both directions)
+  int32_t nsteps;
+  int32_t spin_limit;
+};
+
+// step_tile's view of the forward's arguments (StepArgs' names)
+template <int NP> struct PFwdView {
+  const EOArgs<NP>& op;
+  double sc;
+  int64_t ktot, stride, n0;
+  int32_t K, jend;
+};
+
+template <int NPL, int W, int MS> struct PSGeo {
+  static constexpr int kA = PHGeo<NPL, W>::kLds, kF = TileGeo<NPL, W>::kLds;
+  static constexpr int kLds = (kA > kF ? kA : kF) + MS * 5 + 1;
+};
+
+template <int NPL, bool UNI, int W, int MS>
+__global__ __launch_bounds__(kBlock * W) __attribute__((amdgpu_waves_per_eu(kPFWaves<NPL, UNI>)))
+void k_psweep(PSweepArgs<NPL, MS> a) {
+  using A = PSweepArgs<NPL, MS>;
+  constexpr int NPH = NPL + 1, H = MS * 5, T = kBlock * W, TE = T - 2 * H, NW = T / 64;
+  __shared__ __attribute__((aligned(16))) double lds[PSGeo<NPL, W, MS>::kLds];
+  __shared__ uint32_t s_item, s_epoch, s_last, s_bad;
+  __shared__ double s_av[NW];
+  __shared__ int64_t s_ai[NW];
+  uint32_t* sync = a.sync;
+  uint32_t* flags = sync + dgr::kSyncFlags;
+  const int tid = threadIdx.x;
+  const int nT = a.nT, nb = a.nb;
+  const int64_t nF = int64_t(nb) * nT;
+  const uint64_t t_start = a.trace ? uint64_t(wall_clock64()) : 0;
+  if (tid == 0) {
+    uint32_t it, ep;
+    dgr::flow_take(sync, 2 * nF, &it, &ep);
+    s_item = it;
+    s_epoch = ep;
+    s_bad = 0u;
+  }
+  __syncthreads();
+  const int64_t item = s_item;
+  const uint32_t epoch = s_epoch;
+  const uint64_t t_deq = a.trace ? uint64_t(wall_clock64()) : 0;
+  uint64_t t_ready = 0;
+  const bool fwd = item < nF;
+  const int blk = int((fwd ? item : item - nF) / nT);
+  const int j = int((fwd ? item : item - nF) - int64_t(blk) * nT);
+  const int64_t ktot = a.ktot;
+  // the poll: the previous block's tiles j-1..j+1 of the same direction; estimate block 0:
+  // the last forward block's (items nF - nT ..)
+  const auto wait_producers = [&]() {
+    if ((blk > 0 || !fwd) && tid < 64) {
+      const int lo = j > 0 ? j - 1 : 0, hi = j + 1 < nT ? j + 1 : nT - 1;
+      const int64_t d0 = fwd ? int64_t(blk - 1) * nT : (blk == 0 ? nF - nT : nF + int64_t(blk - 1) * nT);
+      const bool gave_up = dgr::sweep_wait(flags + d0 + lo, hi - lo + 1, epoch, sync, a.err_host,
+                                           a.spin_limit);
+      if (tid == 0 && gave_up) s_bad = 1u;
+    }
+    // no acquire fence: every load of handed-off bytes is an sc1 load; this only keeps the
+    // compiler from hoisting them above the poll
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    if (a.trace) t_ready = uint64_t(wall_clock64());
+  };
+  dgr::EtaSink es;
+  es.argmax = false;
+  es.bv = -INFINITY;  // the weakest candidate (dg_argmax's convention)
+  es.bi = INT64_MAX;
+  const int64_t e0 = int64_t(j) * TE - H;
+  const bool edge = edge_tile(e0, T, ktot, a.K);
+  if (fwd) {
+    wait_producers();
+    const int64_t n0 = int64_t(blk) * MS;
+    const PFwdView<NPL> v{a.fop, a.sc, ktot, a.stride, n0, a.K, 0};
+    const double* kin = a.fuin + blk * (MS * 5 + 1);
+    if (edge)
+      step_tile<NPL, 5, UNI, W, MS, false, true, true>(lds, j, a.snap + n0 * a.stride,
+                                                       a.snap + (n0 + 1) * a.stride, nullptr,
+                                                       a.fscale, v, kin);
+    else
+      step_tile<NPL, 5, UNI, W, MS, false, false, true>(lds, j, a.snap + n0 * a.stride,
+                                                        a.snap + (n0 + 1) * a.stride, nullptr,
+                                                        a.fscale, v, kin);
+    if (s_bad) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int64_t o0 = int64_t(j) * TE * NPL, nd = ktot * NPL;
+      const int64_t cnt = (nd - o0) < int64_t(TE) * NPL ? nd - o0 : int64_t(TE) * NPL;
+      for (int st = 0; st < MS; ++st)
+        dgr::poison_run<T>(a.snap + (n0 + 1 + st) * a.stride, o0, cnt);
+    }
+  } else {
+    const DG_KAS A* ka =
+        reinterpret_cast<const DG_KAS A*>(kernarg_tail_k<decltype(&k_psweep<NPL, UNI, W, MS>), A>());
+    const double* kbnd = reinterpret_cast<const double*>(
+                             kernarg_tail<decltype(&k_psweep<NPL, UNI, W, MS>), A>() +
+                             offsetof(A, bnd)) + blk * (MS * 5 + 1);
+    const int64_t n0 = int64_t(a.nsteps) - int64_t(blk + 1) * MS;
+    const bool lastb = blk == nb - 1;
+    es.eta = a.eta;
+    es.part_out = (a.has_eta && !lastb) ? a.part + int64_t(blk) * ktot : nullptr;
+    es.part_in = a.part;
+    es.part_ld = ktot;
+    es.nparts = lastb ? nb - 1 : 0;
+    es.mode = a.has_eta;
+    es.argmax = lastb && a.am_idx != nullptr;
+    const double* snap = a.snap + n0 * a.stride;
+    const bool term = blk == 0;  // the terminal weight P u^nsteps
+    using WP = decltype(wait_producers);
+    if (edge)
+      adjph_tile<NPL, UNI, W, MS, true, true, true, A, NoWait, true, WP>(
+          lds, j, a.W[blk], a.W[blk + 1], snap, a.eta, a.scale, a, ka, kbnd, term, &es, NoWait(),
+          wait_producers);
+    else
+      adjph_tile<NPL, UNI, W, MS, false, true, true, A, NoWait, true, WP>(
+          lds, j, a.W[blk], a.W[blk + 1], snap, a.eta, a.scale, a, ka, kbnd, term, &es, NoWait(),
+          wait_producers);
+    if (s_bad) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int64_t o0 = int64_t(j) * TE, ndh = ktot * NPH;
+      const int64_t ne = (ktot - o0) < TE ? ktot - o0 : int64_t(TE);
+      dgr::poison_run<T>(a.W[blk + 1], o0 * NPH,
+                         (ndh - o0 * NPH) < int64_t(TE) * NPH ? ndh - o0 * NPH : int64_t(TE) * NPH);
+      if (a.has_eta) dgr::poison_run<T>(es.part_out ? es.part_out : a.eta, o0, ne);
+      es.bv = __builtin_nan("");
+    }
+    if (es.argmax) {
+      dgr::wg_argmax<NW>(es.bv, es.bi, s_av, s_ai);
+      if (tid == 0) {
+        dgr::st8_agent(a.am_pv + j, __builtin_bit_cast(uint64_t, es.bv));
+        dgr::st8_agent(a.am_pi + j, uint64_t(es.bi));
+      }
+    }
+  }
+  const uint64_t t_body = a.trace ? uint64_t(wall_clock64()) : 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) dgr::st_agent(flags + item, epoch);
+  if (es.argmax)
+    dgr::flow_refine_arrive<NW>(sync, nT, a.am_pv, a.am_pi, a.am_idx, a.am_val, a.am_nf, &s_last,
+                                s_av, s_ai);
+  if (a.trace && tid == 0) {
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* tr = a.trace + 8 * item;
+    tr[0] = t_start;
+    tr[1] = t_deq;
+    tr[2] = t_ready;
+    tr[3] = t_body;
+    tr[4] = uint64_t(wall_clock64());
+    tr[5] = (uint64_t(xcc) << 32) | blockIdx.x;
+  }
+}
+
+template <int NPL, int W, int MS>
+int launch_psweep(dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const PFlowBufs& b,
+                  double* snapshots, double* eta, int mode, const double* tn, double dt,
+                  int nsteps, hipStream_t st) {
+  const dgr::RkPoly& P = dgr::rk_poly();
+  if (!P.ok) return fail(DG_ERR_HIP, "LSERK4 stability polynomial: beta_0 = beta_1 = 1 expected");
+  using A = PSweepArgs<NPL, MS>;
+  const int nb = nsteps / MS;
+  if (nb < 2 || nb > A::kMaxBlocks || nb * MS != nsteps)
+    return fail(DG_ERR_ARG, "p sweep dataflow: nsteps must be 2..32/MS blocks of MS steps");
+  A a;
+  make_eo<NPL + 1>(hi, hi->uniform ? dt * hi->s_uniform : 1.0, &a.op, true);
+  a.pr = pr;
+  a.sc = dt;
+  for (int k = 0; k < 6; ++k) a.beta[k] = P.beta[k];
+  make_eo<NPL>(lo, lo->uniform ? dt * lo->s_uniform : 1.0, &a.fop, true);  // as launch_step_e
+  for (int i = 0; i < A::kMaxBlocks * (MS * 5 + 1); ++i) a.bnd[i] = a.fuin[i] = 0.0;
+  for (int bk = 0; bk < nb; ++bk) {
+    const int n0 = nsteps - (bk + 1) * MS;  // estimate block b
+    double bnd[MS * 6 + 1];
+    dgr::rp_block_bnd(lo, MS, &tn[n0], dt, bnd);
+    for (int i = 0; i < MS * 5; ++i) a.bnd[bk * (MS * 5 + 1) + i] = bnd[i];
+    const int f0 = bk * MS;  // forward block b: StepArgs::uin of a launch at t_{f0}
+    double* u = a.fuin + bk * (MS * 5 + 1);
+    for (int m = 0; m < MS; ++m)
+      for (int s = 0; s < 5; ++s) u[m * 5 + s] = inflow_value(lo, tn[f0 + m] + RK<5>::C(s) * dt);
+    u[MS * 5] = inflow_value(lo, tn[f0 + MS]);
+  }
+  a.snap = snapshots;
+  for (int i = 0; i <= A::kMaxBlocks; ++i) a.W[i] = i <= nb ? b.W[i] : nullptr;
+  a.eta = eta;
+  a.part = b.part;
+  a.scale = hi->d_scale;
+  a.fscale = lo->d_scale;
+  a.sync = b.sync;
+  a.err_host = lo->d_sweep_err;
+  a.trace = lo->sweep_trace;
+  a.am_idx = b.am_idx;
+  a.am_val = b.am_val;
+  a.am_nf = b.am_nf;
+  a.am_pv = b.am_pv;
+  a.am_pi = b.am_pi;
+  a.ktot = lo->ktot;
+  a.stride = lo->ktot * NPL;
+  a.K = int32_t(lo->K);
+  a.has_eta = mode;
+  a.nb = nb;
+  a.nT = int(grid_for(lo->ktot, kBlock * W - 2 * MS * 5));
+  a.nsteps = nsteps;
+  a.spin_limit = lo->sweep_spin_limit > 0 ? lo->sweep_spin_limit : dgr::kSweepSpinLimit;
+  const unsigned grid = unsigned(2 * int64_t(nb) * a.nT);
+  if (hi->uniform)
+    hipLaunchKernelGGL((k_psweep<NPL, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_psweep<NPL, false, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, a);
+  HIP_TRY(hipGetLastError());
+  return DG_OK;
+}
+
 // DG_P_HORNER (read once, A/B runs): 0 round 3's stage loop (k_adj_p), 1 Horner (k_adj_ph)
 // with the next snapshot tile prefetched into registers (94 VGPRs at Np = 5: 5 waves per
 // SIMD), 2 Horner pipelined (k_adj_pq: the forward recompute of step n-1 beside the reverse
@@ -822,48 +1085,23 @@ bool p_flow_shape(const dg_plan* lo, int nsteps) {
 // it (unless the terminal weight is formed in the kernel) and the last rewrites it; with
 // nb >= 2 the last block's tile j starts after every first-block tile whose input range
 // overlaps its output range (j-1..j+1, through the chain of waits).
+int p_flow_bufs(dg_plan* lo, const dg_plan* hi, uint64_t tag, int m, int W, int nsteps,
+                int64_t items, int64_t items_cap, int64_t nT, int64_t nT_cap, int nb, double* w,
+                bool eta, int64_t* idx, double* value, int64_t* nonfinite, hipStream_t st,
+                PFlowBufs* b);
+
 int adjp_flow(dg_plan* lo, const dg_plan* hi, const double* P, double* w,
               const double* snapshots, const double* tn, double dt, int nsteps, double* eta,
               int mode, bool term, int64_t* idx, double* value, int64_t* nonfinite,
               hipStream_t st) {
-  if (const int rc = sweep_watchdog(lo)) return rc;
   const int m = p_msteps(lo), nb = nsteps / m, W = lo->p_tile_width;
   const int64_t TE = int64_t(kBlock) * W - 10 * m;
-  const int64_t nT = (lo->ktot + TE - 1) / TE, items = int64_t(nb) * nT;
-  const int64_t kcap = lo->K_cap * lo->batch;
-  const int64_t nT_cap = (kcap + TE - 1) / TE, items_cap = int64_t(nb) * nT_cap;
-  const size_t sync_bytes =
-      (sizeof(uint32_t) * size_t(sweep_sync_words() + items_cap) + 255) & ~size_t(255);
-  const int64_t field_hi = lo->ktot * hi->NP;
-  const size_t fcap = sizeof(double) * size_t(kcap) * size_t(hi->NP);
-  const int nparts = eta ? nb - 1 : 0;
-  const size_t data_bytes = fcap * size_t(nb - 1) + sizeof(double) * size_t(kcap) * size_t(nparts) +
-                            (idx ? 16 * size_t(nT_cap) : 0);
-  char* data = nullptr;
-  if (const int rc = sweep_scratch(lo, sync_bytes, data_bytes, st, &data)) return rc;
-  // the take counter numbers launches by items per launch, the refine's arrival counter by
-  // the last block's tiles: another shape (or the jump sweep on this region) starts afresh
-  const uint64_t sig = uint64_t(items) * 1000003u ^ (uint64_t(0x5a) << 56) ^
-                       (uint64_t(m) << 48) ^ (uint64_t(W) << 40) ^ (uint64_t(nsteps) << 32) ^
-                       uint64_t(nT);
-  if (lo->sweep_items != items || lo->sweep_sig != sig) {
-    HIP_TRY(hipMemsetAsync(lo->d_sweep, 0, sync_bytes, st));
-    lo->sweep_items = items;
-    lo->sweep_sig = sig;
-  }
-  double* fld = reinterpret_cast<double*>(data);
-  PFlowBufs b{};
-  b.W[0] = w;
-  for (int k = 1; k < nb; ++k) b.W[k] = fld + field_hi * (k - 1);
-  b.W[nb] = w;
-  double* rest = fld + field_hi * (nb - 1);
-  b.part = nparts ? rest : nullptr;
-  b.sync = static_cast<uint32_t*>(lo->d_sweep);
-  b.am_idx = idx;
-  b.am_val = value;
-  b.am_nf = nonfinite;
-  b.am_pv = idx ? rest + lo->ktot * nparts : nullptr;
-  b.am_pi = idx ? reinterpret_cast<int64_t*>(b.am_pv + nT) : nullptr;
+  const int64_t nT = (lo->ktot + TE - 1) / TE;
+  const int64_t nT_cap = (lo->K_cap * lo->batch + TE - 1) / TE;
+  PFlowBufs b;
+  if (const int rc = p_flow_bufs(lo, hi, 0x5a, m, W, nsteps, int64_t(nb) * nT, int64_t(nb) * nT_cap,
+                                 nT, nT_cap, nb, w, eta != nullptr, idx, value, nonfinite, st, &b))
+    return rc;
   int rc = DG_OK;
   switch (lo->NP) {
 #define DG_ADJPF_CASE(NPLV)                                                                  \
@@ -884,6 +1122,89 @@ int adjp_flow(dg_plan* lo, const dg_plan* hi, const double* P, double* w,
     DG_ADJPF_CASE(2) DG_ADJPF_CASE(3) DG_ADJPF_CASE(4) DG_ADJPF_CASE(5)
     DG_ADJPF_CASE(6) DG_ADJPF_CASE(7) DG_ADJPF_CASE(8)
 #undef DG_ADJPF_CASE
+    default: return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+  }
+  return rc;
+}
+
+// The whole sweep as one dataflow launch applies: the estimate's dataflow shape at 4-step
+// blocks, the forward's stage-loop workgroup tiles (not the wave tiles of N <= 2), and
+// 2..8 blocks.
+bool p_sweep_shape(const dg_plan* lo, int nsteps) {
+  return lo->p_sweep && p_flow_shape(lo, nsteps) && p_msteps(lo) == 4 && lo->lane_elems == 0 &&
+         lo->nstages == 5 && nsteps <= kPSMaxSteps;
+}
+
+// Scratch and control words of a dataflow launch over `items` work items whose last block has
+// nT tiles (the estimate's), with nb - 1 intermediate order-(N+1) fields and partial rows.
+int p_flow_bufs(dg_plan* lo, const dg_plan* hi, uint64_t tag, int m, int W, int nsteps,
+                int64_t items, int64_t items_cap, int64_t nT, int64_t nT_cap, int nb, double* w,
+                bool eta, int64_t* idx, double* value, int64_t* nonfinite, hipStream_t st,
+                PFlowBufs* b) {
+  if (const int rc = sweep_watchdog(lo)) return rc;
+  const int64_t kcap = lo->K_cap * lo->batch;
+  const size_t sync_bytes =
+      (sizeof(uint32_t) * size_t(sweep_sync_words() + items_cap) + 255) & ~size_t(255);
+  const int64_t field_hi = lo->ktot * hi->NP;
+  const size_t fcap = sizeof(double) * size_t(kcap) * size_t(hi->NP);
+  const int nparts = eta ? nb - 1 : 0;
+  const size_t data_bytes = fcap * size_t(nb - 1) + sizeof(double) * size_t(kcap) * size_t(nparts) +
+                            (idx ? 16 * size_t(nT_cap) : 0);
+  char* data = nullptr;
+  if (const int rc = sweep_scratch(lo, sync_bytes, data_bytes, st, &data)) return rc;
+  // the take counter numbers launches by items per launch, the refine's arrival counter by
+  // the last block's tiles: another shape (or the jump sweep on this region) starts afresh
+  const uint64_t sig = uint64_t(items) * 1000003u ^ (tag << 56) ^ (uint64_t(m) << 48) ^
+                       (uint64_t(W) << 40) ^ (uint64_t(nsteps) << 32) ^ uint64_t(nT);
+  if (lo->sweep_items != items || lo->sweep_sig != sig) {
+    HIP_TRY(hipMemsetAsync(lo->d_sweep, 0, sync_bytes, st));
+    lo->sweep_items = items;
+    lo->sweep_sig = sig;
+  }
+  double* fld = reinterpret_cast<double*>(data);
+  *b = PFlowBufs{};
+  b->W[0] = w;
+  for (int k = 1; k < nb; ++k) b->W[k] = fld + field_hi * (k - 1);
+  b->W[nb] = w;
+  double* rest = fld + field_hi * (nb - 1);
+  b->part = nparts ? rest : nullptr;
+  b->sync = static_cast<uint32_t*>(lo->d_sweep);
+  b->am_idx = idx;
+  b->am_val = value;
+  b->am_nf = nonfinite;
+  b->am_pv = idx ? rest + lo->ktot * nparts : nullptr;
+  b->am_pi = idx ? reinterpret_cast<int64_t*>(b->am_pv + nT) : nullptr;
+  return DG_OK;
+}
+
+// dg_lserk4_sweep_p's one dataflow launch (k_psweep).  Snapshot 0 holds u^0.
+int psweep(dg_plan* lo, const dg_plan* hi, const double* P, double* snapshots, double* w,
+           const double* tn, double dt, int nsteps, double* eta, int mode, int64_t* idx,
+           double* value, int64_t* nonfinite, hipStream_t st) {
+  const int m = 4, nb = nsteps / m, W = lo->p_tile_width;
+  const int64_t TE = int64_t(kBlock) * W - 10 * m;
+  const int64_t nT = (lo->ktot + TE - 1) / TE;
+  const int64_t nT_cap = (lo->K_cap * lo->batch + TE - 1) / TE;
+  PFlowBufs b;
+  if (const int rc = p_flow_bufs(lo, hi, 0x5b, m, W, nsteps, 2 * int64_t(nb) * nT,
+                                 2 * int64_t(nb) * nT_cap, nT, nT_cap, nb, w, eta != nullptr, idx,
+                                 value, nonfinite, st, &b))
+    return rc;
+  int rc = DG_OK;
+  switch (lo->NP) {
+#define DG_PSWEEP_CASE(NPLV)                                                                 \
+    case NPLV: {                                                                             \
+      PrEO<NPLV> pr;                                                                         \
+      if (!make_prolong_eo<NPLV>(P, &pr))                                                    \
+        return fail(DG_ERR_ARG, "P does not commute with the node reversal (symmetric nodes)"); \
+      if (W == 2)                                                                            \
+        rc = launch_psweep<NPLV, 2, 4>(lo, hi, pr, b, snapshots, eta, mode, tn, dt, nsteps, st); \
+      else                                                                                   \
+        rc = launch_psweep<NPLV, 1, 4>(lo, hi, pr, b, snapshots, eta, mode, tn, dt, nsteps, st); \
+    } break;
+    DG_PSWEEP_CASE(2) DG_PSWEEP_CASE(3) DG_PSWEEP_CASE(4) DG_PSWEEP_CASE(5)
+    DG_PSWEEP_CASE(6) DG_PSWEEP_CASE(7) DG_PSWEEP_CASE(8)
+#undef DG_PSWEEP_CASE
     default: return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
   }
   return rc;
@@ -1005,6 +1326,40 @@ int dg_plan_query_p_flow(const dg_plan* lo, int nsteps, int* out) {
   if (!lo || !out) return fail(DG_ERR_ARG, "null argument");
   *out = p_flow_shape(lo, nsteps) ? 1 : 0;
   return DG_OK;
+}
+
+int dg_plan_query_p_sweep(const dg_plan* lo, int nsteps, int* out) {
+  if (!lo || !out) return fail(DG_ERR_ARG, "null argument");
+  *out = p_sweep_shape(lo, nsteps) ? 1 : 0;
+  return DG_OK;
+}
+
+int dg_lserk4_sweep_p(dg_plan* lo, dg_plan* hi, const double* P, double* snapshots, double* w,
+                      double t0, double dt, int nsteps, double* eta, int flags, int64_t* idx,
+                      double* value, int64_t* nonfinite_count, void* stream) {
+  if (!lo || !hi || !P || !snapshots || !w) return fail(DG_ERR_ARG, "null argument");
+  if (idx && !eta) return fail(DG_ERR_ARG, "the refine decision needs eta");
+  if (nsteps < 0) return fail(DG_ERR_ARG, "nsteps < 0");
+  if (flags & ~(DG_ADJ_ETA_ASSIGN | DG_ADJ_ETA_ABS))
+    return fail(DG_ERR_ARG, "unknown flags (the terminal weight is always P u^nsteps)");
+  if (int rc = check_pair(lo, hi)) return rc;
+  if (lo->NP > 8) return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
+  if (!p_sweep_shape(lo, nsteps)) {
+    // the launch chains: the snapshot forward in place from snapshot 0, then the estimate
+    if (const int rc = dg_lserk4_fwd_ex(lo, snapshots, t0, dt, nsteps, snapshots, nullptr, stream))
+      return rc;
+    return adj_p_impl(lo, hi, P, w, snapshots, t0, dt, nsteps, eta,
+                      flags | DG_ADJ_P_TERMINAL_PROLONG, idx, value, nonfinite_count, stream);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  std::vector<double> tn(size_t(nsteps) + 1);  // time = time + dt (One_code.mlx:139)
+  tn[0] = t0;
+  for (int n = 0; n < nsteps; ++n) tn[n + 1] = tn[n] + dt;
+  const int mode = eta ? (kEtaOn | ((flags & DG_ADJ_ETA_ASSIGN) ? kEtaAssign : 0) |
+                          ((flags & DG_ADJ_ETA_ABS) ? kEtaAbs : 0))
+                       : 0;
+  return psweep(lo, hi, P, snapshots, w, tn.data(), dt, nsteps, eta, mode, idx, value,
+                nonfinite_count, st);
 }
 
 }  // extern "C"

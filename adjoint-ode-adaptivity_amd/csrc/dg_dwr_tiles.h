@@ -19,7 +19,7 @@
 // Sources: matlab/MAIN.m:32-34 (adjoint at order Ns+1), matlab/adj_march.m:103-117 (err(k) =
 // v_k' R_k), python/Main_finite_difference.py:79-94 (errEst); DESIGN.md §6c.
 #pragma once
-#include "dg_rec_tiles.h"
+#include "dg_step_tile.h"
 
 namespace dgk {
 
@@ -116,7 +116,8 @@ __device__ __forceinline__ void lds_barrier() {
 // of a wave write 64 consecutive 16-byte slots from M0, the wave's base): no registers held
 // while the loads are in flight.  Interior tiles only (every 16-byte slot in range).  The
 // image is complete after `s_waitcnt vmcnt(0)` and a barrier.  Returns the image offset.
-template <int NP, int W>
+// AUX: the cache-policy bits (dgr::kSc1 for bytes written earlier in the same launch).
+template <int NP, int W, int AUX = 0>
 __device__ __forceinline__ int tile_issue_lds(const double* __restrict__ g, int64_t e0,
                                               double* __restrict__ lds) {
   using G = TileGeo<NP, W>;
@@ -132,39 +133,10 @@ __device__ __forceinline__ int tile_issue_lds(const double* __restrict__ g, int6
   for (int q = 0; q < G::kVec; ++q) {
     const int v = threadIdx.x + q * G::LB;
     if (v < nvec)
-      __builtin_amdgcn_global_load_lds((glb_void*)(gb + 2 * v), (lds_void*)(lds + 2 * (q * G::LB + wb)),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void*)(gb + 2 * v),
+                                       (lds_void*)(lds + 2 * (q * G::LB + wb)), 16, 0, AUX);
   }
   return off;
-}
-
-// tile_issue with sc1 loads (dg_rec_tiles.h tile_load's WT policy): the input of a work item
-// of a dataflow launch, written write-through by an earlier item of the same launch.
-template <int NP, int W, bool EDGE>
-__device__ __forceinline__ void tile_issue_wt(const double* __restrict__ g, int64_t e0,
-                                              int64_t nd, TileRegs<NP, W>& r) {
-  using G = TileGeo<NP, W>;
-  const int64_t d0 = e0 * NP;
-  const int64_t base = d0 & ~int64_t(1);
-  r.off = int(d0 - base);
-  const int nvec = (G::T * NP + r.off + 1) >> 1;
-  const int64_t bc = base > 0 ? base : 0;  // (base < 0 only in edge tiles: those lanes load nothing)
-  const __amdgpu_buffer_rsrc_t rs = dgr::wt_rsrc(g + bc);
-#pragma unroll
-  for (int q = 0; q < G::kVec; ++q) {
-    const int v = threadIdx.x + q * G::LB;
-    const int64_t gd = base + 2 * int64_t(v);
-    double2 val = make_double2(0.0, 0.0);
-    if (v < nvec) {
-      if (!EDGE || (gd >= 0 && gd + 1 < nd)) {
-        val = dgr::wt_ld16(rs, uint32_t(gd - bc) * 8u);
-      } else {
-        if (gd >= 0 && gd < nd) val.x = dgr::wt_ld8(rs, uint32_t(gd - bc) * 8u);
-        if (gd + 1 >= 0 && gd + 1 < nd) val.y = dgr::wt_ld8(rs, uint32_t(gd + 1 - bc) * 8u);
-      }
-    }
-    r.v[q] = val;
-  }
 }
 
 // One element's indicator in a dataflow launch (rp_adj_tile's WT branch): a block other than
@@ -215,13 +187,15 @@ template <int NPL, int W> struct PHGeo {
 // block), as the jump sweep's rp_adj_tile does.  A: the argument struct (op, pr, sc, beta,
 // ktot, stride, K, has_eta).  term: the terminal weight is P u^{n0+MS} (win is not read).
 // wait_inputs: called by all threads once the snapshot loads are issued, before w is loaded
-// (a dataflow item's poll of its producers and the barrier after it).
+// (a dataflow item's poll of its producers and the barrier after it); wait_snapshots: before
+// the snapshot loads.  SWT: the snapshots are loaded sc1 (written earlier in the same launch).
 struct NoWait {
   __device__ void operator()() const {}
 };
 
 template <int NPL, bool UNI, int W, int MS, bool EDGE, bool GL = false, bool WT = false,
-          class A = AdjPHArgs<NPL, MS>, class WaitF = NoWait>
+          class A = AdjPHArgs<NPL, MS>, class WaitF = NoWait, bool SWT = false,
+          class WaitS = NoWait>
 __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t tile,
                                            const double* __restrict__ win,
                                            double* __restrict__ wout,
@@ -231,7 +205,9 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
                                            const A& args, const DG_KAS A* ka,
                                            const double* kbnd, bool term,
                                            dgr::EtaSink* es = nullptr,
-                                           const WaitF& wait_inputs = WaitF()) {
+                                           const WaitF& wait_inputs = WaitF(),
+                                           const WaitS& wait_snapshots = WaitS()) {
+  static_assert(!SWT || GL, "sc1 snapshot loads: direct-to-LDS tiles only");
   constexpr int NPH = NPL + 1;
   using G = PHGeo<NPL, W>;
   constexpr int T = G::T, LB = G::LB;
@@ -254,8 +230,14 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
   TileRegs<NPL, W> pa, pb;
   // the snapshots (an earlier launch's) are loaded while a dataflow item waits for its
   // producers (wait_inputs), then w
-  tile_issue<NPL, W, EDGE>(snap + MS * args.stride, e0, ndl, pa);
-  tile_issue<NPL, W, EDGE>(snap + (MS - 1) * args.stride, e0, ndl, pb);
+  wait_snapshots();  // (SWT: the snapshots are this launch's: their producers first)
+  if constexpr (SWT) {
+    tile_issue_wt<NPL, W, EDGE>(snap + MS * args.stride, e0, ndl, pa);
+    tile_issue_wt<NPL, W, EDGE>(snap + (MS - 1) * args.stride, e0, ndl, pb);
+  } else {
+    tile_issue<NPL, W, EDGE>(snap + MS * args.stride, e0, ndl, pa);
+    tile_issue<NPL, W, EDGE>(snap + (MS - 1) * args.stride, e0, ndl, pb);
+  }
   wait_inputs();
   if (!term) {
     if constexpr (WT) tile_issue_wt<NPH, W, EDGE>(win, e0, ndh, pw);
@@ -406,7 +388,8 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
     constexpr bool kGL = GL && !EDGE;
     int offn = 0;
     if constexpr (kGL) {
-      if (st > 0) offn = tile_issue_lds<NPL, W>(snap + (st - 1) * args.stride, e0, lds);
+      if (st > 0)
+        offn = tile_issue_lds<NPL, W, SWT ? dgr::kSc1 : 0>(snap + (st - 1) * args.stride, e0, lds);
     } else if constexpr (!GL) {
       if (st > 0) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
     }
@@ -507,7 +490,8 @@ __device__ __forceinline__ void adjph_tile(double* __restrict__ lds, int64_t til
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         off = offn;
       } else {
-        if constexpr (GL) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
+        if constexpr (GL && SWT) tile_issue_wt<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
+        else if constexpr (GL) tile_issue<NPL, W, EDGE>(snap + (st - 1) * args.stride, e0, ndl, pa);
         tile_commit<NPL, W>(pa, lds);
         off = pa.off;
       }

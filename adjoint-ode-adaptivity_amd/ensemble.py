@@ -95,9 +95,10 @@ class EnsembleSweep:
         self.est = DWREstimate(self.op)
         self.w = self.est.new_field()
         if self.op.N >= 3:
-          # its forward keeps every state: the stage-loop step on pair tiles, 8 steps per
-          # launch on 1024-element tiles (84.4 us per launch, profiles/r05/p; the Horner-form
-          # pair step with register snapshot stores, snap_pairs=1, took 108.2 us)
+          # where the sweep is not one dataflow launch (p_sweep) its forward keeps every
+          # state in launches of the stage-loop step, 8 steps per launch on 512-element tiles
+          # (88 us per launch, profiles/r05/p; the Horner-form pair step with register
+          # snapshot stores, snap_pairs=1, took 108 us)
           self.op.tune(tile_width=2, steps_per_launch=8)
       else:
         # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
@@ -156,6 +157,10 @@ class EnsembleSweep:
     if self.record == "jumps":
       self.op.sweep_rec(self.u0, self.jumps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
                         eta_assign=True, eta_abs=True, terminal_state=True)
+    elif self.p_sweep:
+      # the p-estimate's whole sweep as one dataflow launch (dg_lserk4_sweep_p)
+      self.est.sweep(self.snaps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
+                     eta_assign=True, eta_abs=True)
     else:
       self.forward()
       self.adjoint()
@@ -173,8 +178,13 @@ class EnsembleSweep:
     idx = reducer.idx if idx is None else idx
     value = reducer.value if value is None else value
     if self.est is not None:
-      # the p-estimate: the snapshot forward, then the estimate with the refine decision
-      # (fused into its dataflow launch where the shape allows, dg_lserk4_adj_p_refine)
+      if self.p_sweep:  # forward + estimate + refine decision in one dataflow launch
+        self.est.sweep(self.snaps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
+                       eta_assign=True, eta_abs=True, idx=idx, value=value,
+                       nonfinite=reducer.nonfinite)
+        return
+      # the snapshot forward, then the estimate with the refine decision (fused into its
+      # dataflow launch where the shape allows, dg_lserk4_adj_p_refine)
       self.forward()
       self.estimate_refine(idx, value, reducer.nonfinite)
       return
@@ -192,6 +202,12 @@ class EnsembleSweep:
     """True when the p-estimate runs as ONE dataflow launch (dg_lserk4_adj_p, DG_TUNE_P_FLOW)."""
     return self.est is not None and self.est.query_flow(self.nsteps)
 
+  @property
+  def p_sweep(self):
+    """True when the p-estimate's forward and estimate run as ONE dataflow launch
+    (dg_lserk4_sweep_p: the forward's 4-step blocks are the estimate's)."""
+    return self.est is not None and self.est.query_sweep(self.nsteps)
+
   def capture(self):
     """Capture the sweep as HIP graphs (replayed by sweep_graph, or forward_graph /
     adjoint_graph for the two halves of the snapshot pair): the per-launch host work
@@ -204,7 +220,7 @@ class EnsembleSweep:
       self.sweep()
     torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize(dev)
-    if self.dataflow:
+    if self.dataflow or self.p_sweep:
       g = torch.cuda.CUDAGraph()
       with torch.cuda.graph(g):
         self.sweep()

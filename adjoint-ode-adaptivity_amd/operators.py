@@ -535,12 +535,15 @@ class DWREstimate:
     self._P, self._P_ptr = _lib.dbl_array(self.P)
     self.tune(tile_width, steps_per_launch)
 
-  def tune(self, tile_width=None, steps_per_launch=None, flow=None):
+  def tune(self, tile_width=None, steps_per_launch=None, flow=None, sweep=None):
     """Tiles of 256*``tile_width`` elements (1, 2) and ``steps_per_launch`` (1, 2, 4; 8 on
     512-element tiles) reverse steps per launch of dg_lserk4_adj_p; ``flow`` (0 / 1): one
     launch per block, or the whole estimate as one dataflow launch where the steps split
-    into 2 or more blocks of 4 (or 8 on 512-element tiles) steps (bit-identical)."""
+    into 2 or more blocks of 4 (or 8 on 512-element tiles) steps (bit-identical); ``sweep``
+    (0 / 1): ``sweep`` as the chains or as one dataflow launch (bit-identical)."""
     lib, plan = self.lo._lib, self.lo._plan
+    if sweep is not None:
+      _lib.check(lib.dg_plan_tune(plan, _lib.DG_TUNE_P_SWEEP, int(sweep)), "dg_plan_tune")
     if flow is not None:
       _lib.check(lib.dg_plan_tune(plan, _lib.DG_TUNE_P_FLOW, int(flow)), "dg_plan_tune")
     if tile_width is not None:
@@ -559,6 +562,41 @@ class DWREstimate:
     _lib.check(self.lo._lib.dg_plan_query_p_flow(self.lo._plan, int(nsteps), ctypes.byref(out)),
                "dg_plan_query_p_flow")
     return bool(out.value)
+
+  def query_sweep(self, nsteps):
+    """True if ``sweep`` over ``nsteps`` steps runs forward and estimate as one dataflow
+    launch (dg_lserk4_sweep_p)."""
+    out = ctypes.c_int32()
+    _lib.check(self.lo._lib.dg_plan_query_p_sweep(self.lo._plan, int(nsteps), ctypes.byref(out)),
+               "dg_plan_query_p_sweep")
+    return bool(out.value)
+
+  def sweep(self, snapshots, w, t0, dt, nsteps, eta=None, eta_assign=True, eta_abs=True,
+            idx=None, value=None, nonfinite=None):
+    """The whole p sweep (dg_lserk4_sweep_p): the order-N forward from ``snapshots[0]`` (u^0)
+    into ``snapshots[1..nsteps]``, then the estimate with the terminal weight P u^nsteps into
+    ``w`` (order N+1, swept back to t_0) and ``eta``; with ``idx`` also the refine decision
+    (as ``estimate_refine``).  One dataflow launch where ``query_sweep`` says so, else the
+    launch chains; bit-identical to ``lo.forward`` at 4 steps per launch + ``estimate``."""
+    def p1(t, dtype, name):
+      if t is None:
+        return None
+      if isinstance(t, int):  # a device address (host_alias of pinned host memory)
+        return ctypes.c_void_p(t)
+      if not t.is_cuda or t.dtype != dtype or t.numel() < 1:
+        raise TypeError(f"{name} must be a CUDA {dtype} tensor or a device address")
+      return ctypes.c_void_p(t.data_ptr())
+    eta_p = None if eta is None else self.lo._field(eta, "eta", self.lo.ktot)
+    flags = ((_lib.DG_ADJ_ETA_ASSIGN if eta_assign else 0) |
+             (_lib.DG_ADJ_ETA_ABS if eta_abs else 0))
+    rc = self.lo._lib.dg_lserk4_sweep_p(
+        self.lo._plan, self.hi._plan, self._P_ptr,
+        self.lo._field(snapshots, "snapshots", (nsteps + 1) * self.lo.field_numel),
+        self.hi._field(w, "w"), float(t0), float(dt), int(nsteps), eta_p, int(flags),
+        p1(idx, torch.int64, "idx"), p1(value, torch.float64, "value"),
+        p1(nonfinite, torch.int64, "nonfinite"), _stream(self.lo.device))
+    _lib.check(rc, "dg_lserk4_sweep_p")
+    return w, eta
 
   def new_field(self, count=None):
     return self.hi.new_field(count)

@@ -679,6 +679,8 @@ def main(argv=None):
   # forward's launches; with one trajectory on one rank its last block reduces the refine
   # decision too (dg_lserk4_adj_p_refine)
   pflow = args.indicator == "p" and sweep.p_dataflow
+  # ... and its forward with it: the whole p sweep as ONE dataflow launch (dg_lserk4_sweep_p)
+  psweep = args.indicator == "p" and sweep.p_sweep
   fused_refine = ((dataflow or pflow) and world == 1 and sweep.batch == 1 and not args.gather_ics
                   and not args.graph)
   # The refine index (the mesh split's input) and the indicator there go to the host in one
@@ -695,6 +697,16 @@ def main(argv=None):
   def one_step(ev=None):
     if ev:
       ev[0].record(stream)
+    if fused_refine and psweep:  # forward + estimate + refine decision: one launch
+      if res_alias is not None:
+        sweep.sweep_refine(reducer, idx=res_alias, value=res_alias + 8)
+      else:
+        sweep.sweep_refine(reducer)
+      if ev:
+        ev[2].record(stream)
+      if res_alias is None:
+        copy_result()
+      return
     if fused_refine and pflow:
       sweep.forward()
       if ev:
@@ -719,7 +731,7 @@ def main(argv=None):
       if res_alias is None:
         copy_result()
       return
-    if dataflow:
+    if dataflow or psweep:
       sweep.sweep_graph() if args.graph else sweep.sweep()
       if ev:
         ev[2].record(stream)
@@ -783,7 +795,9 @@ def main(argv=None):
     ms, tw = ((sweep.est.steps_per_launch, sweep.est.tile_width) if pmode
               else (fms, sweep.op.tile_width))
   chunks, fchunks = sweep_chunks(nsteps, ms), sweep_chunks(nsteps, fms)
-  if dataflow:  # one launch per sweep: its time, reported in the adjoint's slot
+  if psweep:  # the forward runs in the estimate's 4-step blocks inside the one launch
+    fms, fchunks = ms, list(chunks)
+  if dataflow or psweep:  # one launch per sweep: its time, reported in the adjoint's slot
     fwd_us = [float("nan") for e in evs]
     adj_us = [e[0].elapsed_time(e[2]) * 1e3 for e in evs]
   else:
@@ -815,9 +829,12 @@ def main(argv=None):
     fwd_bytes = float(np.mean([(16.0 * Np + 8.0 * m) * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 * Np + 8.0 * m + 16.0) * ktot for m in chunks]))
   elif pmode:
-    fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
+    agg = np.sum if psweep else np.mean
+    fwd_bytes = float(agg([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
     adj_bytes = float((np.sum if pflow else np.mean)(
         [(16.0 * (Np + 1) + 8.0 * (m + 1) * Np + 16.0) * ktot for m in chunks]))
+    if psweep:  # the one launch moves both directions' bytes
+      adj_bytes += fwd_bytes
   else:
     fwd_bytes = float(np.mean([(8.0 + 8.0 * m) * Np * ktot for m in fchunks]))
     adj_bytes = float(np.mean([(16.0 + 8.0 * m) * Np * ktot + 16.0 * ktot for m in chunks]))
@@ -825,7 +842,7 @@ def main(argv=None):
   pairs = args.record == "jumps" and getattr(sweep.op, "rec_lane_elements", 1) == 2
   kadj, kstep = ("k_adj_rp", "k_step_rp") if pairs else ("k_adj", "k_step")
   if pmode:
-    kadj = "k_adjp_flow" if pflow else "k_adj_p"
+    kadj = "k_psweep" if psweep else "k_adjp_flow" if pflow else "k_adj_p"
   if dataflow:
     kadj = "k_sweep_rp"
   tile_tag = tile_tag_fwd = f"{tw},2 elements/lane" if pairs else f"{tw}"
@@ -847,7 +864,7 @@ def main(argv=None):
   else:
     # the snapshot forward runs on 256-element one-wave tiles (4 elements per lane) at N <= 2
     # by default (dg_plan_create), else on workgroup tiles of 256 * tile width
-    T_fwd = 256 if N <= 2 else 256 * sweep.op.tile_width
+    T_fwd = 256 * tw if psweep else 256 if N <= 2 else 256 * sweep.op.tile_width
     T_of = lambda m, fwd: T_fwd if fwd else 256 * tw  # noqa: E731
     h_fwd = h_adj = lambda m: 5 * m  # noqa: E731
   halo_adj = float(np.average([halo_factor(T_of(m, False), h_adj(m)) for m in chunks],
@@ -875,7 +892,8 @@ def main(argv=None):
       continue
     if (tr.get("N") == N and tr.get("K") == K and tr.get("batch") == sweep.batch
         and tr.get("steps_per_launch") == ms and bool(tr.get("dataflow")) == dataflow
-        and bool(tr.get("p_flow")) == pflow and (not pmode or tr.get("tile_width", tw) == tw)
+        and bool(tr.get("p_flow")) == pflow and bool(tr.get("p_sweep")) == psweep
+        and (not pmode or tr.get("tile_width", tw) == tw)
         and tr.get("record", "snapshots") == args.record
         and tr.get("indicator", "jump") == args.indicator
         and same_kernel(tr)):
@@ -920,7 +938,7 @@ def main(argv=None):
   fwd_fpu = horner_flops_per_update(Np, False) if horner else eo_flops_per_update(Np, False)
   adj_tf = adj_fpu * upl / (adj_launch_us * 1e-6) / 1e12
   fwd_tf = fwd_fpu * fupl / (fwd_launch_us * 1e-6) / 1e12
-  if dataflow:
+  if dataflow or psweep:
     # the one launch executes both directions' flops; its issued lanes weight each
     # direction's halo factor by its share of them
     f_fl, a_fl = fwd_fpu * Np * ktot * nsteps, adj_fpu * Np * ktot * nsteps
@@ -1019,12 +1037,39 @@ def main(argv=None):
         fl = sq["fp64_flops_issued_per_launch"]
         f["pmc_issued_per_launch"] = fl
         f["pmc_issued_frac"] = fl / (adj_launch_us * 1e-6) / 1e12 / FP64_PEAK_TFLOPS
-        f["pmc_issued_over_useful"] = fl / (adj_fpu * upl)
+        f["pmc_issued_over_useful"] = fl / (((fwd_fpu + adj_fpu) * Np * ktot * nsteps) if psweep
+                                            else adj_fpu * upl)
         f["pmc_wait_any_frac"] = sq.get("wait_any_frac_of_wave_cycles")
         f["pmc_source"] = os.path.relpath(os.path.join(prof_dir, "sq_summary.json"), ROOT)
     except (OSError, ValueError, KeyError, TypeError):
       pass
-  if pflow:
+  if psweep:
+    r = out["roofline"]
+    r["kernel"] = (f"k_psweep<{Np - 1}+1,uniform,{256 * tw} elements,{ms} steps per block> "
+                   f"(ONE dataflow launch per sweep: {len(fchunks)} forward blocks + "
+                   f"{len(chunks)} estimate blocks of {ms} steps + DWR"
+                   f"{' + refine decision' if fused_refine else ''})")
+    r["note"] = ("the p sweep as one dataflow launch (dg_lserk4_sweep_p): the order-N snapshot "
+                 "forward's and the estimate's blocks are the work items; algorithmic bytes = "
+                 "both directions' blocks; per reverse step the order-(N+1) forward step from "
+                 "the prolonged snapshot and the order-(N+1) reverse step (roofline_fp64)")
+    out["roofline_fwd"] = None
+    f = out["roofline_fp64"]
+    for k in ("fwd_achieved", "fwd_frac", "fwd_issued_frac"):
+      f[k] = None
+    f["what"] = ("algorithmic fp64 flops of both directions (interior elements) per launch / "
+                 "launch time; adj_issued_frac weights each direction's halo by its flops")
+    out["stream_copy"]["fwd_frac_of_achievable"] = None
+    out["p_dataflow"] = {"launches_per_sweep": 1, "blocks_fwd": fchunks, "blocks": chunks,
+                         "refine_in_launch": fused_refine,
+                         "refine_to_host": ("written by the launch into pinned memory "
+                                            "(dg_host_alias)" if res_alias is not None
+                                            else "async copy"),
+                         "work_items": 2 * len(chunks) * -(-ktot // (256 * tw - 10 * ms)),
+                         "status": sweep.op.sweep_status()}
+    if out["p_dataflow"]["status"]:
+      raise RuntimeError("a p-sweep work item gave up waiting for a producer")
+  elif pflow:
     r = out["roofline"]
     r["kernel"] = (f"k_adjp_flow<{Np - 1}+1,uniform,{256 * tw} elements,{ms} steps per block> "
                    f"(ONE dataflow launch per estimate: {len(chunks)} blocks of {ms} reverse "

@@ -148,12 +148,15 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             watchdog) when nsteps splits into 2 .. 40/steps-per-launch blocks
  *                             of the plan's steps per launch; 0 one launch per block.
  *                             Bit-identical results
+ *   DG_TUNE_P_SWEEP           dg_lserk4_sweep_p: 1 (default) runs the snapshot forward and the
+ *                             estimate as ONE dataflow launch where dg_plan_query_p_sweep
+ *                             allows; 0 the chains.  Bit-identical results
  *   DG_TUNE_SWEEP_SPIN_LIMIT  diagnostics/tests: polls a dataflow work item makes before it
  *                             gives up waiting for a producer (0: the default, ~2^20; 1 makes
  *                             the watchdog fire on any multi-block sweep)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
  * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
- * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE, DG_SNAP_PAIRS, DG_P_FLOW. */
+ * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE, DG_SNAP_PAIRS, DG_P_FLOW, DG_P_SWEEP. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
@@ -161,7 +164,7 @@ enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER =
        DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12,
        DG_TUNE_SWEEP_SPIN_LIMIT = 13, DG_TUNE_SWEEP_WAVES = 14,
        DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16, DG_TUNE_SWEEP_EXCHANGE = 17,
-       DG_TUNE_SNAP_PAIRS = 18, DG_TUNE_P_FLOW = 19 };
+       DG_TUNE_SNAP_PAIRS = 18, DG_TUNE_P_FLOW = 19, DG_TUNE_P_SWEEP = 20 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
@@ -389,6 +392,23 @@ int dg_lserk4_adj_p_refine(dg_plan* lo, dg_plan* hi, const double* P, double* w,
  * current settings (DG_TUNE_P_FLOW, steps per launch 4, or 8 on 512-element tiles, 2..40/MS
  * blocks), else 0. */
 int dg_plan_query_p_flow(const dg_plan* lo, int nsteps, int* out);
+
+/* The p-estimate's whole sweep: the order-N LSERK4 forward from snapshot 0 (u^0, the caller's)
+ * writing snapshots 1..nsteps, then dg_lserk4_adj_p with the terminal weight P u^nsteps
+ * (DG_ADJ_P_TERMINAL_PROLONG implied) and, with idx non-null, the refine decision as
+ * dg_lserk4_adj_p_refine.  Where the shape allows (dg_plan_query_p_sweep: the dataflow
+ * estimate at 4-step blocks, the forward's workgroup tiles, 2..8 blocks) both directions run
+ * as ONE dataflow launch (k_psweep: forward blocks then estimate blocks as work items), else
+ * as dg_lserk4_fwd_ex + dg_lserk4_adj_p(_refine).  Bit-identical to dg_lserk4_fwd_ex with
+ * the lo plan's steps per launch at 4 followed by dg_lserk4_adj_p.  flags: DG_ADJ_ETA_ASSIGN /
+ * _ABS.  Replaces the reference's forward march + adjoint march + error estimate
+ * (matlab/MAIN.m:32-34, adj_march.m:103-117). */
+int dg_lserk4_sweep_p(dg_plan* lo, dg_plan* hi, const double* P, double* snapshots, double* w,
+                      double t0, double dt, int nsteps, double* eta, int flags, int64_t* idx,
+                      double* value, int64_t* nonfinite_count, void* stream);
+
+/* *out = 1 if dg_lserk4_sweep_p over nsteps steps runs as one dataflow launch, else 0. */
+int dg_plan_query_p_sweep(const dg_plan* lo, int nsteps, int* out);
 
 /* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */

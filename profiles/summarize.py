@@ -75,11 +75,14 @@ def main():
       return keys, sum(hbm(k) * out[k]["fetch_dispatches"] for k in keys) / n
 
     adj, adj_b = sweep_mean("k_adj_p" if a.indicator == "p" else "k_adj")
-    p_flow = False
+    p_flow = p_sweep = False
     if a.indicator == "p":
       pf, pf_b = sweep_mean("k_adjp_flow")
       if pf:  # the p-estimate as one dataflow launch
         adj, adj_b, p_flow = pf, pf_b, True
+      ps, ps_b = sweep_mean("k_psweep")
+      if ps:  # the whole p sweep as one dataflow launch: both directions' traffic
+        adj, adj_b, fwd, fwd_b, p_flow, p_sweep = ps, ps_b, [], None, True, True
     fwd, fwd_b = sweep_mean("k_step")
     dataflow = False
     sw, sw_b = sweep_mean("k_sweep_rp")
@@ -87,6 +90,7 @@ def main():
       adj, adj_b, fwd, fwd_b, dataflow = sw, sw_b, [], None, True
     tr = {"N": a.N, "K": a.K, "batch": a.batch, "steps_per_launch": a.steps_per_launch,
           "record": a.record, "indicator": a.indicator, "dataflow": dataflow, "p_flow": p_flow,
+          "p_sweep": p_sweep,
           "tile_width": a.tile_width, "source": a.out,
           "adj_kernel": adj, "adj_bytes_per_launch": adj_b,
           "fwd_kernel": fwd, "fwd_bytes_per_launch": fwd_b,
