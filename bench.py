@@ -804,7 +804,6 @@ def main(argv=None):
     fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / len(fchunks) for e in evs]
     # the p-estimate's one dataflow launch: its whole time (its blocks are not separate)
     adj_us = [e[3].elapsed_time(e[2]) * 1e3 / (1 if pflow else len(chunks)) for e in evs]
-  prolong_us = [e[1].elapsed_time(e[3]) * 1e3 for e in evs] if pmode else None
   step_ms = [evs[i][0].elapsed_time(evs[i + 1][0] if i + 1 < len(evs) else ev_end)
              for i in range(len(evs))]
   fwd_launch_us, adj_launch_us = float(np.mean(fwd_us)), float(np.mean(adj_us))
@@ -1028,7 +1027,6 @@ def main(argv=None):
                   "override": bool(os.environ.get("DG_LIB_PATH"))},
   }
   if pmode:
-    out["prolong_us"] = float(np.mean(prolong_us))
     try:  # issued fp64 of k_adj_p from the SQ passes of the same bench (profiles/r04/p/)
       with open(os.path.join(prof_dir, "sq_summary.json")) as fh:
         sq = json.load(fh)
