@@ -19,4 +19,10 @@ for f in ("gpurun_out/r05/final/bench.json", "gpurun_out/r05/final/bench_p.json"
 t = json.load(open("gpurun_out/r05/p/pmc_traffic.json")); print({k: t.get(k) for k in ("adj_kernel", "adj_bytes_per_launch", "p_flow", "p_sweep", "tile_width")})
 s = json.load(open("gpurun_out/r05/p/sq_summary.json")); print(s["kernel"], s["wait_any_frac_of_wave_cycles"], s["fp64_flops_issued_per_launch"])
 PY
-echo all-done
+echo main-done
+# A/B: two queue items per workgroup in the p sweep launch (k_psweep2, DG_P_SWEEP_PAIR=1)
+DG_P_SWEEP_PAIR=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_psweep.py > $out/pytest_pair.log 2>&1; rc=$?
+tail -2 $out/pytest_pair.log
+[ $rc -eq 0 ] || exit 1
+bash profiles/r05/ab_env.sh $out/ab_pair "--indicator p" "DG_P_SWEEP_PAIR=0" "DG_P_SWEEP_PAIR=1" || exit 1
+echo pair-done
