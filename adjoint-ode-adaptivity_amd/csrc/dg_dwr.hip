@@ -940,199 +940,6 @@ void k_psweep(PSweepArgs<NPL, MS> a) {
   }
 }
 
-// k_psweep with two queue items per workgroup (DG_P_SWEEP_PAIR=1, A/B): one take and one
-// poll cover both (the item overhead is a third of a forward item, a fifth of an estimate
-// item); a unit never mixes the directions, so each loop carries one body's constants.
-template <int NPL, bool UNI, int W, int MS>
-__global__ __launch_bounds__(kBlock * W) __attribute__((amdgpu_waves_per_eu(kPFWaves<NPL, UNI>)))
-void k_psweep2(PSweepArgs<NPL, MS> a) {
-  using A = PSweepArgs<NPL, MS>;
-  constexpr int NPH = NPL + 1, H = MS * 5, T = kBlock * W, TE = T - 2 * H, NW = T / 64;
-  __shared__ __attribute__((aligned(16))) double lds[PSGeo<NPL, W, MS>::kLds];
-  __shared__ uint32_t s_unit, s_epoch, s_last, s_bad;
-  __shared__ double s_av[NW];
-  __shared__ int64_t s_ai[NW];
-  uint32_t* sync = a.sync;
-  uint32_t* flags = sync + dgr::kSyncFlags;
-  const int tid = threadIdx.x;
-  const int nT = a.nT, nb = a.nb;
-  const int64_t nF = int64_t(nb) * nT;
-  const int64_t nUF = (nF + 1) / 2, nU = 2 * nUF;  // forward units, then as many estimate units
-  uint64_t t_start = a.trace ? uint64_t(wall_clock64()) : 0;
-  if (tid == 0) {
-    uint32_t u, ep;
-    dgr::flow_take(sync, nU, &u, &ep);
-    s_unit = u;
-    s_epoch = ep;
-    s_bad = 0u;
-  }
-  __syncthreads();
-  const int64_t unit = s_unit;
-  const uint32_t epoch = s_epoch;
-  uint64_t t_deq = a.trace ? uint64_t(wall_clock64()) : 0;
-  const bool fwd = unit < nUF;
-  const int64_t i0 = fwd ? 2 * unit : nF + 2 * (unit - nUF);  // the unit's first item
-  const int64_t iend = fwd ? nF : 2 * nF;
-  const int64_t ktot = a.ktot;
-  uint64_t t_ready = 0;
-  {  // one poll for both items: lanes 0..31 the first item's producers, 32..63 the second's
-    if (tid < 64) {
-      const int k = tid >> 5, l = tid & 31;
-      const int64_t item = i0 + k;
-      const uint32_t* f = nullptr;
-      if (item < iend) {
-        const int64_t r = fwd ? item : item - nF;
-        const int blk = int(r / nT), j = int(r - int64_t(blk) * nT);
-        if (blk > 0 || !fwd) {
-          const int lo = j > 0 ? j - 1 : 0, hi = j + 1 < nT ? j + 1 : nT - 1;
-          const int64_t d0 = fwd ? int64_t(blk - 1) * nT
-                                 : (blk == 0 ? nF - nT : nF + int64_t(blk - 1) * nT);
-          const int64_t q = d0 + lo + l;
-          if (l <= hi - lo && q < i0) f = flags + q;  // (the unit's own first item runs first)
-        }
-      }
-      bool ok = f == nullptr;
-      if (!ok) ok = dgr::ld_agent(f) == epoch;
-      int spins = 0;
-      bool gave_up = false;
-      while (!__all(ok)) {
-        __builtin_amdgcn_s_sleep(2);
-        if (!ok) ok = dgr::ld_agent(f) == epoch;
-        if (++spins >= a.spin_limit) {
-          if (tid == 0) {
-            dgr::st_agent(sync + dgr::kSyncErr, 1u);
-            if (a.err_host)
-              __hip_atomic_store(a.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-          gave_up = true;
-          break;
-        }
-        if ((spins & 255) == 0 && dgr::ld_agent(sync + dgr::kSyncErr) != 0u) {
-          gave_up = true;
-          break;
-        }
-      }
-      if (tid == 0 && gave_up) s_bad = 1u;
-    }
-    // no acquire fence: every load of handed-off bytes is an sc1 load; this only keeps the
-    // compiler from hoisting them above the poll
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __syncthreads();
-    if (a.trace) t_ready = uint64_t(wall_clock64());
-  }
-  const auto publish = [&](int64_t item, uint64_t t_body) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) dgr::st_agent(flags + item, epoch);
-    if (a.trace && tid == 0) {
-      uint32_t xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      uint64_t* tr = a.trace + 8 * item;
-      const uint64_t now = uint64_t(wall_clock64());
-      tr[0] = t_start;
-      tr[1] = t_deq;
-      tr[2] = t_ready;
-      tr[3] = t_body;
-      tr[4] = now;
-      tr[5] = (uint64_t(xcc) << 32) | blockIdx.x;
-      t_start = t_deq = t_ready = now;
-    }
-  };
-  if (fwd) {
-#pragma unroll 1
-    for (int k = 0; k < 2; ++k) {
-      const int64_t item = i0 + k;
-      if (item >= iend) break;
-      const int blk = int(item / nT), j = int(item - int64_t(blk) * nT);
-      const int64_t e0 = int64_t(j) * TE - H;
-      const int64_t n0 = int64_t(blk) * MS;
-      const PFwdView<NPL> v{a.fop, a.sc, ktot, a.stride, n0, a.K, 0};
-      const double* kin = a.fuin + blk * (MS * 5 + 1);
-      if (edge_tile(e0, T, ktot, a.K))
-        step_tile<NPL, 5, UNI, W, MS, false, true, true>(lds, j, a.snap + n0 * a.stride,
-                                                         a.snap + (n0 + 1) * a.stride, nullptr,
-                                                         a.fscale, v, kin);
-      else
-        step_tile<NPL, 5, UNI, W, MS, false, false, true>(lds, j, a.snap + n0 * a.stride,
-                                                          a.snap + (n0 + 1) * a.stride, nullptr,
-                                                          a.fscale, v, kin);
-      if (s_bad) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const int64_t o0 = int64_t(j) * TE * NPL, nd = ktot * NPL;
-        const int64_t cnt = (nd - o0) < int64_t(TE) * NPL ? nd - o0 : int64_t(TE) * NPL;
-        for (int st = 0; st < MS; ++st)
-          dgr::poison_run<T>(a.snap + (n0 + 1 + st) * a.stride, o0, cnt);
-      }
-      publish(item, a.trace ? uint64_t(wall_clock64()) : 0);
-    }
-  } else {
-#pragma unroll 1
-    for (int k = 0; k < 2; ++k) {
-      const int64_t item = i0 + k;
-      if (item >= iend) break;
-      const int64_t r = item - nF;
-      const int blk = int(r / nT), j = int(r - int64_t(blk) * nT);
-      const int64_t e0 = int64_t(j) * TE - H;
-      const DG_KAS A* ka = reinterpret_cast<const DG_KAS A*>(
-          kernarg_tail_k<decltype(&k_psweep2<NPL, UNI, W, MS>), A>());
-      const double* kbnd = reinterpret_cast<const double*>(
-                               kernarg_tail<decltype(&k_psweep2<NPL, UNI, W, MS>), A>() +
-                               offsetof(A, bnd)) + blk * (MS * 5 + 1);
-      const int64_t n0 = int64_t(a.nsteps) - int64_t(blk + 1) * MS;
-      const bool lastb = blk == nb - 1;
-      dgr::EtaSink es;
-      es.eta = a.eta;
-      es.part_out = (a.has_eta && !lastb) ? a.part + int64_t(blk) * ktot : nullptr;
-      es.part_in = a.part;
-      es.part_ld = ktot;
-      es.nparts = lastb ? nb - 1 : 0;
-      es.mode = a.has_eta;
-      es.argmax = lastb && a.am_idx != nullptr;
-      es.bv = -INFINITY;
-      es.bi = INT64_MAX;
-      const double* snap = a.snap + n0 * a.stride;
-      const bool term = blk == 0;
-      if (edge_tile(e0, T, ktot, a.K))
-        adjph_tile<NPL, UNI, W, MS, true, true, true, A, NoWait, true>(
-            lds, j, a.W[blk], a.W[blk + 1], snap, a.eta, a.scale, a, ka, kbnd, term, &es);
-      else
-        adjph_tile<NPL, UNI, W, MS, false, true, true, A, NoWait, true>(
-            lds, j, a.W[blk], a.W[blk + 1], snap, a.eta, a.scale, a, ka, kbnd, term, &es);
-      if (s_bad) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const int64_t o0 = int64_t(j) * TE, ndh = ktot * NPH;
-        const int64_t ne = (ktot - o0) < TE ? ktot - o0 : int64_t(TE);
-        dgr::poison_run<T>(a.W[blk + 1], o0 * NPH,
-                           (ndh - o0 * NPH) < int64_t(TE) * NPH ? ndh - o0 * NPH
-                                                                : int64_t(TE) * NPH);
-        if (a.has_eta) dgr::poison_run<T>(es.part_out ? es.part_out : a.eta, o0, ne);
-        es.bv = __builtin_nan("");
-      }
-      if (es.argmax) {
-        dgr::wg_argmax<NW>(es.bv, es.bi, s_av, s_ai);
-        if (tid == 0) {
-          dgr::st8_agent(a.am_pv + j, __builtin_bit_cast(uint64_t, es.bv));
-          dgr::st8_agent(a.am_pi + j, uint64_t(es.bi));
-        }
-      }
-      publish(item, a.trace ? uint64_t(wall_clock64()) : 0);
-      if (es.argmax)
-        dgr::flow_refine_arrive<NW>(sync, nT, a.am_pv, a.am_pi, a.am_idx, a.am_val, a.am_nf,
-                                    &s_last, s_av, s_ai);
-    }
-  }
-}
-
-inline bool p_sweep_pair() {
-  static const bool v = [] {
-    const char* e = std::getenv("DG_P_SWEEP_PAIR");
-    return e && std::atoi(e) == 1;
-  }();
-  return v;
-}
-
 template <int NPL, int W, int MS>
 int launch_psweep(dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const PFlowBufs& b,
                   double* snapshots, double* eta, int mode, const double* tn, double dt,
@@ -1183,15 +990,6 @@ int launch_psweep(dg_plan* lo, const dg_plan* hi, const PrEO<NPL>& pr, const PFl
   a.nT = int(grid_for(lo->ktot, kBlock * W - 2 * MS * 5));
   a.nsteps = nsteps;
   a.spin_limit = lo->sweep_spin_limit > 0 ? lo->sweep_spin_limit : dgr::kSweepSpinLimit;
-  if (p_sweep_pair()) {
-    const unsigned grid2 = unsigned(2 * ((int64_t(nb) * a.nT + 1) / 2));
-    if (hi->uniform)
-      hipLaunchKernelGGL((k_psweep2<NPL, true, W, MS>), dim3(grid2), dim3(kBlock * W), 0, st, a);
-    else
-      hipLaunchKernelGGL((k_psweep2<NPL, false, W, MS>), dim3(grid2), dim3(kBlock * W), 0, st, a);
-    HIP_TRY(hipGetLastError());
-    return DG_OK;
-  }
   const unsigned grid = unsigned(2 * int64_t(nb) * a.nT);
   if (hi->uniform)
     hipLaunchKernelGGL((k_psweep<NPL, true, W, MS>), dim3(grid), dim3(kBlock * W), 0, st, a);

@@ -22,7 +22,7 @@ snaps = op.new_field(n + 1)
 op.init_sine([1.0], [1.0], [0.0], out=snaps[0])
 w = est.new_field()
 eta = torch.zeros(op.ktot, dtype=torch.float64, device="cuda")
-TE = 256 * tw - 20
+TE = 256 * tw - 2 * 5 * 4  # 4-step blocks: a halo of 20 elements per side
 nT = -(-op.ktot // TE)
 nb = n // 4
 items = 2 * nb * nT

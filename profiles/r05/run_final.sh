@@ -20,7 +20,8 @@ t = json.load(open("gpurun_out/r05/p/pmc_traffic.json")); print({k: t.get(k) for
 s = json.load(open("gpurun_out/r05/p/sq_summary.json")); print(s["kernel"], s["wait_any_frac_of_wave_cycles"], s["fp64_flops_issued_per_launch"])
 PY
 echo main-done
-# A/B: two queue items per workgroup in the p sweep launch (k_psweep2, DG_P_SWEEP_PAIR=1)
+# A/B (round 5, since removed): two queue items per workgroup in the p sweep launch
+# (k_psweep2, DG_P_SWEEP_PAIR=1)
 DG_P_SWEEP_PAIR=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_psweep.py > $out/pytest_pair.log 2>&1; rc=$?
 tail -2 $out/pytest_pair.log
 [ $rc -eq 0 ] || exit 1

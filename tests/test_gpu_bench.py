@@ -60,17 +60,20 @@ def test_bench_single_rank_line(gpu, dataflow):
 
 
 def test_bench_p_estimate_line(gpu):
-  """--indicator p: the forward keeps snapshots, the adjoint is k_adj_p (order N+1 + the
-  prolonged one-step residual); its line carries the same roofline blocks and a CPU baseline
-  of the oracle's p-estimate."""
+  """--indicator p: the forward keeps snapshots and the estimate runs at order N+1 with the
+  prolonged one-step residual -- by default both as ONE dataflow launch (k_psweep, with the
+  refine decision); its line carries the same roofline blocks and a CPU baseline of the
+  oracle's p-estimate."""
   out = _run(["--K", "65536", "--steps", "3", "--warmup", "2", "--no-converge",
               "--cpu-steps", "2"])
   assert out["indicator"] == "jump"
   out = _run(["--K", "65536", "--steps", "3", "--warmup", "2", "--no-converge",
               "--indicator", "p", "--cpu-steps", "2"])
   assert out["indicator"] == "p" and out["config"]["record"] == "snapshots"
-  assert out["roofline"]["kernel"].startswith("k_adj_p<5")
-  assert 0 < out["roofline"]["frac"] < 1 and out["prolong_us"] > 0
+  assert out["roofline"]["kernel"].startswith("k_psweep<4+1")
+  assert out["p_dataflow"]["launches_per_sweep"] == 1 and out["p_dataflow"]["status"] == 0
+  assert out["p_dataflow"]["refine_in_launch"]
+  assert 0 < out["roofline"]["frac"] < 1
   assert out["nonfinite_indicator_steps"] == 0
   assert out["cpu_baseline"]["value"] > 0 and "p-enriched" in out["cpu_baseline"]["sample"]
 
