@@ -78,7 +78,7 @@ def test_bench_p_estimate_line(gpu):
   assert out["cpu_baseline"]["value"] > 0 and "p-enriched" in out["cpu_baseline"]["sample"]
 
 
-@pytest.mark.parametrize("extra", [[], ["--ics", "6"]])
+@pytest.mark.parametrize("extra", [[], ["--ics", "6"], ["--indicator", "p"]])
 def test_bench_self_launches_two_ranks(gpu, extra):
   out = _run(["--gpus", "2", "--backend", "gloo", "--K", "65536", "--steps", "2",
               "--warmup", "1", "--no-converge", "--no-cpu-baseline", *extra])
@@ -86,6 +86,9 @@ def test_bench_self_launches_two_ranks(gpu, extra):
   assert out["collective_backend"] == "gloo"  # never reported as RCCL when gloo ran
   ranks = out["refine_index_ranks"]
   assert len(ranks) == 2 and ranks[0] == ranks[1] == out["refine_index"]
-  if extra:
+  if extra and extra[0] == "--indicator":  # the p sweep's one launch per rank, no fused refine
+    assert out["indicator"] == "p" and out["p_dataflow"]["launches_per_sweep"] == 1
+    assert not out["p_dataflow"]["refine_in_launch"] and out["p_dataflow"]["status"] == 0
+  elif extra:
     assert out["scaling"] == "strong" and out["config"]["trajectories"] == 6
     assert out["config"]["trajectories_per_gpu"] == 3
