@@ -296,12 +296,50 @@ def test_effectivity_table_on_the_gpu(pkg, gpu, N, K):
 
 @pytest.mark.slow
 def test_full_size_p_estimate(pkg, gpu):
-  """The p-estimate at config 2's size (N = 4, K = 2^20): 4 steps of the
-  order-N forward with snapshots, then dg_lserk4_adj_p from a seeded order-(N+1) terminal
-  weight, against oracle.effectivity.p_estimate on the GPU's own snapshots -- the whole
-  mesh (the oracle's numpy operators finish in seconds at this size) -- for eta and w^0 at
-  1e-10 of max|oracle|, plus the refine index (numpy's argmax of |eta|).  The IC is a sine
-  plus per-node noise so the residual is resolved (see test_gpu_full_size.py)."""
+  """The p sweep at config 2's size (N = 4, K = 2^20) through the path the
+  bench times: ONE dataflow launch of the order-N snapshot forward, the estimate with the
+  terminal weight P u^N and the refine decision (dg_lserk4_sweep_p, 8 steps = 2 + 2 blocks),
+  against oracle.effectivity.p_estimate on the launch's own snapshots -- the whole mesh --
+  for eta and w^0 at 1e-10 of max|oracle|, and the fused refine index against numpy's
+  argmax of the oracle's |eta|.  The terminal weight handed to the oracle is dg_prolong of
+  snapshot N (bit-identical to the in-launch one: test_terminal_prolong_equals_prolong_first).
+  The IC is a sine plus per-node noise so the residual is resolved."""
+  import torch
+  ops = pkg.operators
+  N, K, nsteps = 4, 1 << 20, 8
+  v_x = np.linspace(0.0, 1.0, K + 1)
+  S = setup1d.startup1d(N, v_x, metric="element")
+  S_hi = setup1d.startup1d(N + 1, v_x, metric="element")
+  op = ops.DGAdvection1D(pkg.BaseGalerkin1D(n=N, v_x=v_x), a=A)
+  est = ops.DWREstimate(op)
+  assert (est.tile_width, est.steps_per_launch) == (2, 4)  # the default launch shape (round 5)
+  assert est.query_sweep(nsteps)
+  dt = oadv.bench_dt(S)
+  rng = np.random.default_rng(21)
+  u0 = np.sin(2 * np.pi * S["x"]) + 0.1 * rng.standard_normal(S["x"].shape)
+  snaps = op.new_field(nsteps + 1)
+  snaps[0].copy_(dev(setup1d.to_elem_major(u0), gpu))
+  w = est.new_field()
+  eta = torch.empty(K, dtype=torch.float64, device=gpu)
+  res = torch.zeros(3, dtype=torch.int64, device=gpu)
+  est.sweep(snaps, w, 0.0, dt, nsteps, eta=eta, eta_assign=True, eta_abs=False, idx=res[0:1],
+            value=res[1:2].view(torch.float64), nonfinite=res[2:3])
+  g = setup1d.from_elem_major(host(est.prolong(snaps[nsteps])), N + 2)
+  torch.cuda.synchronize()
+  gs = [setup1d.from_elem_major(host(snaps[n]), N + 1) for n in range(nsteps + 1)]
+  eta_ref, w0_ref = ef.p_estimate(gs, times_of(0.0, dt, nsteps), dt, A, S, S_hi, g, "a")
+  out = [(host(eta), eta_ref, setup1d.from_elem_major(host(w), N + 2), w0_ref)]
+  check(out)
+  a = np.sort(np.abs(eta_ref))
+  assert a[-1] - a[-2] > 1e3 * RTOL * a[-1]
+  assert int(host(res)[0]) == int(np.argmax(np.abs(eta_ref))) and int(host(res)[2]) == 0
+  assert op.sweep_status() == 0
+
+
+@pytest.mark.slow
+def test_full_size_p_estimate_chain(pkg, gpu):
+  """The estimate alone at config 2's size through the launch chain (4 steps: one block):
+  dg_lserk4_adj_p from a seeded order-(N+1) terminal weight against the oracle, as round 4."""
   out, est = run_case(pkg, gpu, 4, 1 << 20, 4, seed=21)
   assert (est.tile_width, est.steps_per_launch) == (2, 4)  # the default launch shape (round 5)
   check(out)
