@@ -80,6 +80,8 @@ def assert_same(a, b, what):
     (6, 600, 1, 1, 4, 8),      # Np = 7, 8: no occupancy cap
     (7, 500, 2, 2, 8, 16),
     (4, 40, 1, 1, 4, 8),       # the whole mesh inside one (edge) tile
+    (4, 777, 1, 2, 4, 12),     # K Np odd: snapshots off 16-byte alignment (direct-to-LDS loads)
+    (2, 1001, 1, 1, 4, 8),
 ])
 def test_flow_equals_chain(pkg, gpu, N, K, batch, tw, spl, nsteps):
   op, est, snaps, w0, dt = setup(pkg, gpu, N, K, batch, seed=N + K, nsteps=nsteps)

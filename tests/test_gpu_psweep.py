@@ -86,6 +86,8 @@ def assert_same(a, b, what):
     (6, 700, 2, 1, 8),
     (7, 500, 1, 2, 12),
     (4, 60, 1, 2, 8),       # the whole mesh inside one (edge) tile
+    (4, 777, 1, 2, 8),      # K Np odd: every other snapshot starts 8 bytes off 16-byte alignment
+    (3, 1001, 3, 1, 12),
 ])
 def test_psweep_equals_chains(pkg, gpu, N, K, batch, tw, nsteps):
   op, est, u0, dt = setup(pkg, gpu, N, K, batch, seed=N + K, tw=tw)
