@@ -32,6 +32,7 @@ DG_TUNE_SWEEP_EXCHANGE = 17
 DG_TUNE_SNAP_PAIRS = 18
 DG_TUNE_P_FLOW = 19
 DG_TUNE_P_SWEEP = 20
+DG_TUNE_NL_EXCHANGE = 21
 DG_FLUX_LINEAR, DG_FLUX_BURGERS = 0, 1
 DG_LIMIT_NONE, DG_LIMIT_EACH_STAGE, DG_LIMIT_PI1_EACH_STAGE = 0, 1, 2
 DG_ADJ_ETA_ASSIGN, DG_ADJ_ETA_ABS = 1, 2
@@ -88,6 +89,7 @@ SIGNATURES = {
                                       ctypes.c_double, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "dg_plan_query_p_flow": (_i32, [_vp, _i32, ctypes.POINTER(_i32)]),
     "dg_plan_query_p_sweep": (_i32, [_vp, _i32, ctypes.POINTER(_i32)]),
+    "dg_plan_query_p_trace": (_i32, [_vp, _i32, _vp]),
     "dg_lserk4_sweep_p": (_i32, [_vp, _vp, _c_dbl_p, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                  _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "dg_slope_limit_n": (_i32, [_vp, _vp, _vp, _vp, _vp]),

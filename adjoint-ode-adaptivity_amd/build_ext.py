@@ -10,7 +10,7 @@ import subprocess
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = [os.path.join(_HERE, "csrc", f) for f in ("dg_advec.hip", "dg_burgers.hip", "dg_wave.hip", "dg_time.hip", "dg_fd.hip",
+SRCS = [os.path.join(_HERE, "csrc", f) for f in ("dg_advec.hip", "dg_burgers.hip", "dg_burgers_ov.hip", "dg_wave.hip", "dg_time.hip", "dg_fd.hip",
                                                      "dg_util.hip", "dg_rec.hip", "dg_dwr.hip",
                                                      "dg_sweep.hip", "dg_sweep_hi.hip",
                                                      "dg_sweep_ov.hip")]

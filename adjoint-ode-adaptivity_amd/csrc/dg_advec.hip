@@ -1245,6 +1245,10 @@ int dg_plan_create(int N, int64_t K, int64_t batch, const double* r, const doubl
     const int k = std::atoi(v);
     if (k == 0 || k == 1) p->sweep_exchange = k;
   }
+  if (const char* v = std::getenv("DG_NL_EXCHANGE")) {
+    const int e = std::atoi(v);
+    if (e == 0 || e == 1) p->nl_exchange = e;
+  }
   if (const char* v = std::getenv("DG_SWEEP_WAVES")) {
     const int k = std::atoi(v);
     if (k == 0 || k == 4 || k == 8 || k == 12 || (k == 16 && p->NP <= 5)) p->sweep_waves = k;
@@ -1406,6 +1410,11 @@ int dg_plan_tune(dg_plan* p, int key, int64_t value) {
       if (value != 0 && value != 1)
         return fail(DG_ERR_ARG, "sweep exchange: 0 (LDS + barrier per level) or 1 (overlapped waves)");
       p->sweep_exchange = int(value);
+      return DG_OK;
+    case DG_TUNE_NL_EXCHANGE:
+      if (value != 0 && value != 1)
+        return fail(DG_ERR_ARG, "config-3 exchange: 0 (workgroup tiles, LDS) or 1 (overlapped waves)");
+      p->nl_exchange = int(value);
       return DG_OK;
     case DG_TUNE_SWEEP_SPIN_LIMIT:
       if (value < 0 || value > (1 << 30)) return fail(DG_ERR_ARG, "spin limit: 0 (default) .. 2^30");

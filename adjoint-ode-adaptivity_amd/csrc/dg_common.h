@@ -93,6 +93,10 @@ __device__ __forceinline__ const DG_KAS char* kernarg_tail_k() {
   return (const DG_KAS char*)__builtin_amdgcn_kernarg_segment_ptr() + KernargLayout<F>::kTailOffset;
 }
 
+// The kernel-argument segment's size limit: launches that pass their constants by value
+// (the dataflow sweeps' block tables) check their argument struct against it at compile time.
+constexpr size_t kKernargMax = 4096;
+
 // Sets the calling thread's dg_last_error() text and returns `code` (dg_advec.hip).
 int fail(int code, const std::string& msg);
 
@@ -497,6 +501,10 @@ struct dg_plan {
   // Horner level (dg_rec_tiles.h), 1 overlapped waves: DPP within a wave, one LDS exchange and
   // barrier per step (dg_ovl_tiles.h)
   int sweep_exchange = 0;
+  // how the config-3 kernels (nonlinear flux / per-stage limiter, dg_burgers*.hip) exchange
+  // neighbour values: 0 workgroup tiles through LDS, a barrier per exchange (dg_burgers.hip);
+  // 1 overlapped waves, DPP shifts, no barrier inside a step (dg_burgers_ov.hip)
+  int nl_exchange = 0;
   // dg_lserk4_fwd with snapshots: 0 the stage-loop kernels (k_step / wave tiles; bit-identical
   // to the record sweeps' stage-loop kernels), 1 Horner-form pair tiles (k_step_rps, dg_rec.hip;
   // tiles of 512 * tile_width elements, msteps steps per launch)

@@ -561,6 +561,7 @@ __global__ __launch_bounds__(kBlock * W) __attribute__((amdgpu_waves_per_eu(kPFW
 void k_adjp_flow(AdjPFArgs<NPL, MS> a) {
   using G = PHGeo<NPL, W>;
   using A = AdjPFArgs<NPL, MS>;
+  static_assert(sizeof(A) <= kKernargMax, "k_adjp_flow's arguments exceed the kernarg segment");
   constexpr int NPH = NPL + 1, H = MS * 5, TE = G::T - 2 * H, NW = kBlock * W / 64;
   __shared__ __attribute__((aligned(16))) double lds[G::kLds + MS * 5 + 1];
   __shared__ uint32_t s_item, s_epoch, s_last, s_bad;
@@ -806,6 +807,7 @@ template <int NPL, bool UNI, int W, int MS>
 __global__ __launch_bounds__(kBlock * W) __attribute__((amdgpu_waves_per_eu(kPFWaves<NPL, UNI>)))
 void k_psweep(PSweepArgs<NPL, MS> a) {
   using A = PSweepArgs<NPL, MS>;
+  static_assert(sizeof(A) <= kKernargMax, "k_psweep's arguments exceed the kernarg segment");
   constexpr int NPH = NPL + 1, H = MS * 5, T = kBlock * W, TE = T - 2 * H, NW = T / 64;
   __shared__ __attribute__((aligned(16))) double lds[PSGeo<NPL, W, MS>::kLds];
   __shared__ uint32_t s_item, s_epoch, s_last, s_bad;
@@ -1334,6 +1336,25 @@ int dg_plan_query_p_sweep(const dg_plan* lo, int nsteps, int* out) {
   return DG_OK;
 }
 
+int dg_plan_query_p_trace(const dg_plan* lo, int nsteps, int64_t out[3]) {
+  if (!lo || !out) return fail(DG_ERR_ARG, "null argument");
+  // work items of each launch (k_adjp_flow: blocks x tiles; k_psweep: twice, forward and
+  // estimate blocks), as adjp_flow / psweep size them
+  const int W = lo->p_tile_width;
+  out[0] = out[1] = 0;
+  if (p_flow_shape(lo, nsteps)) {
+    const int m = p_msteps(lo);
+    const int64_t TE = int64_t(kBlock) * W - 10 * m;
+    out[0] = int64_t(nsteps / m) * ((lo->ktot + TE - 1) / TE);
+  }
+  if (p_sweep_shape(lo, nsteps)) {
+    const int64_t TE = int64_t(kBlock) * W - 10 * 4;
+    out[1] = 2 * int64_t(nsteps / 4) * ((lo->ktot + TE - 1) / TE);
+  }
+  out[2] = 8;  // trace words per item
+  return DG_OK;
+}
+
 int dg_lserk4_sweep_p(dg_plan* lo, dg_plan* hi, const double* P, double* snapshots, double* w,
                       double t0, double dt, int nsteps, double* eta, int flags, int64_t* idx,
                       double* value, int64_t* nonfinite_count, void* stream) {
@@ -1345,9 +1366,18 @@ int dg_lserk4_sweep_p(dg_plan* lo, dg_plan* hi, const double* P, double* snapsho
   if (int rc = check_pair(lo, hi)) return rc;
   if (lo->NP > 8) return fail(DG_ERR_ARG, "the p-estimate supports N <= 7");
   if (!p_sweep_shape(lo, nsteps)) {
-    // the launch chains: the snapshot forward in place from snapshot 0, then the estimate
-    if (const int rc = dg_lserk4_fwd_ex(lo, snapshots, t0, dt, nsteps, snapshots, nullptr, stream))
-      return rc;
+    // the launch chains: the snapshot forward in place from snapshot 0 -- on the stage-loop
+    // workgroup tiles at 4 steps per launch, the dataflow launch's forward blocks, so that the
+    // result does not depend on whether nsteps fits that launch -- then the estimate
+    const int ms = lo->msteps, sp = lo->snap_pairs, le = lo->lane_elems;
+    lo->msteps = 4;
+    lo->snap_pairs = 0;
+    lo->lane_elems = 0;
+    const int rf = dg_lserk4_fwd_ex(lo, snapshots, t0, dt, nsteps, snapshots, nullptr, stream);
+    lo->msteps = ms;
+    lo->snap_pairs = sp;
+    lo->lane_elems = le;
+    if (rf) return rf;
     return adj_p_impl(lo, hi, P, w, snapshots, t0, dt, nsteps, eta,
                       flags | DG_ADJ_P_TERMINAL_PROLONG, idx, value, nonfinite_count, stream);
   }

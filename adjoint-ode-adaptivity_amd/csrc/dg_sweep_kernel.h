@@ -101,6 +101,8 @@ template <int NP, bool UNI, int NW, int MSF, int MSA, int E, int X>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
     E == 2 ? SweepOcc<NP, UNI, NW, X>::waves_per_simd : 1))) void k_sweep_rp(SweepArgs<NP, MSF> a) {
   static_assert(X == 0 || E == 2, "overlapped waves hold element pairs");
+  static_assert(sizeof(SweepArgs<NP, MSF>) <= kKernargMax,
+                "k_sweep_rp's arguments exceed the kernarg segment");
   using G = SwGeo<NP, NW, E, X>;
   constexpr int HF = RpHalo<MSF>::F, HA = RpHalo<MSA>::A;
   constexpr int TEF = G::T - 2 * HF, TEA = G::T - 2 * HA;

@@ -95,10 +95,11 @@ class EnsembleSweep:
         self.est = DWREstimate(self.op)
         self.w = self.est.new_field()
         if self.op.N >= 3:
-          # where the sweep is not one dataflow launch (p_sweep) its forward keeps every
-          # state in launches of the stage-loop step, 8 steps per launch on 512-element tiles
-          # (88 us per launch, profiles/r05/p; the Horner-form pair step with register
-          # snapshot stores, snap_pairs=1, took 108 us)
+          # a separate ``forward`` (the bench's pflow path with the whole-sweep launch tuned
+          # off) keeps every state in launches of the stage-loop step, 8 steps per launch on
+          # 512-element tiles (88 us per launch, profiles/r05/p; the Horner-form pair step with
+          # register snapshot stores, snap_pairs=1, took 108 us); ``sweep`` / ``sweep_refine``
+          # run the forward at 4 steps per launch whatever this says (dg_lserk4_sweep_p)
           self.op.tune(tile_width=2, steps_per_launch=8)
       else:
         # J = |u^N|^2 / 2: the terminal adjoint is u^N itself, so the adjoint sweep runs in
@@ -157,8 +158,10 @@ class EnsembleSweep:
     if self.record == "jumps":
       self.op.sweep_rec(self.u0, self.jumps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
                         eta_assign=True, eta_abs=True, terminal_state=True)
-    elif self.p_sweep:
-      # the p-estimate's whole sweep as one dataflow launch (dg_lserk4_sweep_p)
+    elif self.est is not None:
+      # the p-estimate's whole sweep (dg_lserk4_sweep_p): one dataflow launch where the shape
+      # allows (p_sweep), else the chains with the forward at the launch's 4-step blocks --
+      # the same bits either way, whatever nsteps
       self.est.sweep(self.snaps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
                      eta_assign=True, eta_abs=True)
     else:
@@ -178,15 +181,11 @@ class EnsembleSweep:
     idx = reducer.idx if idx is None else idx
     value = reducer.value if value is None else value
     if self.est is not None:
-      if self.p_sweep:  # forward + estimate + refine decision in one dataflow launch
-        self.est.sweep(self.snaps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
-                       eta_assign=True, eta_abs=True, idx=idx, value=value,
-                       nonfinite=reducer.nonfinite)
-        return
-      # the snapshot forward, then the estimate with the refine decision (fused into its
-      # dataflow launch where the shape allows, dg_lserk4_adj_p_refine)
-      self.forward()
-      self.estimate_refine(idx, value, reducer.nonfinite)
+      # forward + estimate + refine decision (dg_lserk4_sweep_p): one dataflow launch where
+      # the shape allows, else the chains at the same 4-step forward blocks
+      self.est.sweep(self.snaps, self.w, 0.0, self.dt, self.nsteps, eta=self.eta,
+                     eta_assign=True, eta_abs=True, idx=idx, value=value,
+                     nonfinite=reducer.nonfinite)
       return
     self.op.sweep_refine(self.u0, self.jumps, self.w, 0.0, self.dt, self.nsteps, self.eta,
                          idx, value, reducer.nonfinite)

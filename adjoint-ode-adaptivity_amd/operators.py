@@ -138,7 +138,7 @@ class DGAdvection1D:
            rec_tile_width=None, rec_steps_per_launch=None, rec_lane_elements=None,
            rec_fwd_steps_per_launch=None, rec_fwd_tile_width=None, rec_sweep=None,
            sweep_waves=None, sweep_lane_elements=None, sweep_take=None, sweep_exchange=None,
-           snap_pairs=None):
+           snap_pairs=None, nl_exchange=None):
     """Shape of the fused step kernels: tiles of 256*``tile_width`` elements (1 or 2; one
     element per lane), ``steps_per_launch`` (1, 2, 4, or 8 on 512-element tiles) time steps
     fused per launch, and
@@ -162,7 +162,9 @@ class DGAdvection1D:
     LDS exchange and barrier per step (tiles of waves * 116 + 12 elements; bit-identical);
     ``snap_pairs`` (0 / 1): ``forward`` with snapshots on the stage-loop kernels or on
     Horner-form pair tiles (512 * ``tile_width`` elements, ``steps_per_launch`` steps per
-    launch; equal to rounding)."""
+    launch; equal to rounding).  ``nl_exchange`` (0 / 1): the config-3 kernels (``flux`` /
+    ``limiter``) on workgroup tiles exchanging through LDS with a barrier per exchange, or on
+    overlapped waves exchanging by DPP with no barrier inside a step (bit-identical)."""
     for key, val in ((_lib.DG_TUNE_REC_TILE_WIDTH, rec_tile_width),
                      (_lib.DG_TUNE_REC_SWEEP, rec_sweep),
                      (_lib.DG_TUNE_REC_STEPS_PER_LAUNCH, rec_steps_per_launch),
@@ -173,7 +175,8 @@ class DGAdvection1D:
                      (_lib.DG_TUNE_SWEEP_LANE_ELEMENTS, sweep_lane_elements),
                      (_lib.DG_TUNE_SWEEP_TAKE, sweep_take),
                      (_lib.DG_TUNE_SWEEP_EXCHANGE, sweep_exchange),
-                     (_lib.DG_TUNE_SNAP_PAIRS, snap_pairs)):
+                     (_lib.DG_TUNE_SNAP_PAIRS, snap_pairs),
+                     (_lib.DG_TUNE_NL_EXCHANGE, nl_exchange)):
       if val is not None:
         _lib.check(self._lib.dg_plan_tune(self._plan, key, int(val)), "dg_plan_tune")
     if xcd_order is not None:
@@ -404,7 +407,8 @@ class DGAdvection1D:
   def sweep_trace(self, trace):
     """Profiling: record per work item of every later dataflow sweep {taken, producers done,
     published (wall clock, 100 MHz), XCC id << 32 | workgroup} into ``trace`` (CUDA int64,
-    4 * ``query_sweep(nsteps)[3]`` entries); None turns it off."""
+    4 * ``query_sweep(nsteps)[3]`` entries for the jump sweep; the p launches write 8 per
+    item: size it with ``DWREstimate.trace_words``); None turns it off."""
     ptr = None
     if trace is not None:
       if not trace.is_cuda or trace.dtype != torch.int64 or not trace.is_contiguous():
@@ -570,6 +574,15 @@ class DWREstimate:
     _lib.check(self.lo._lib.dg_plan_query_p_sweep(self.lo._plan, int(nsteps), ctypes.byref(out)),
                "dg_plan_query_p_sweep")
     return bool(out.value)
+
+  def trace_words(self, nsteps):
+    """uint64 words a per-item trace (``DGAdvection1D.sweep_trace`` on the lo plan) needs for
+    this estimate's dataflow launches over ``nsteps``: 8 per work item of ``estimate``'s or
+    ``sweep``'s launch, whichever is larger (dg_plan_query_p_trace); 0 if neither is one."""
+    q = (ctypes.c_int64 * 3)()
+    _lib.check(self.lo._lib.dg_plan_query_p_trace(self.lo._plan, int(nsteps), q),
+               "dg_plan_query_p_trace")
+    return int(q[2]) * max(int(q[0]), int(q[1]))
 
   def sweep(self, snapshots, w, t0, dt, nsteps, eta=None, eta_assign=True, eta_abs=True,
             idx=None, value=None, nonfinite=None):

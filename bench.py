@@ -588,7 +588,8 @@ def refine_margin(sweep, step_fn):
   rounding alone moves |eta| by.  That floor is measured, not modelled: the same sweep is run
   once more with the forward in a different block shape (same algorithm, states rounded at
   other steps -- 20-step vs 10-step forward blocks for the jump record, 4 vs 2 steps per
-  launch for snapshots), and the floor is max |eta - eta_alt|.  Run after the timed region;
+  launch for snapshots, for the p estimate a separate 2-step-launch forward and then the
+  estimate instead of the sweep's 4-step forward blocks), and the floor is max |eta - eta_alt|.  Run after the timed region;
   the plan's shape is restored.  One trajectory per rank only (the headline); else None."""
   import torch
   if sweep.batch != 1:
@@ -600,18 +601,32 @@ def refine_margin(sweep, step_fn):
     top = torch.topk(a, 2)
     v1, v2 = float(top.values[0]), float(top.values[1])
     i1, i2 = int(top.indices[0]), int(top.indices[1])
+    alt_fn = step_fn
     if sweep.record == "jumps":
       cur = op.rec_fwd_steps_per_launch
       alt = 10 if cur != 10 else 5
       op.tune(rec_fwd_steps_per_launch=alt)
       shape = (f"forward blocks of {alt} steps instead of {cur}"
                if sweep.nsteps % alt == 0 else None)
+    elif sweep.est is not None:
+      # the p estimate's sweep (dg_lserk4_sweep_p) runs its forward in 4-step blocks whatever
+      # the plan's steps per launch: the alternate pass is a separate snapshot forward in
+      # 2-step launches, then the estimate
+      cur = op.steps_per_launch
+      alt = 2
+      op.tune(steps_per_launch=alt)
+      shape = (f"a separate snapshot forward in launches of {alt} steps, then the estimate, "
+               f"instead of the sweep's 4-step forward blocks")
+
+      def alt_fn():
+        sweep.forward()
+        sweep.run_adjoint()
     else:
       cur = op.steps_per_launch
       alt = 2 if cur != 2 else 1
       op.tune(steps_per_launch=alt)
       shape = f"forward launches of {alt} steps instead of {cur}"
-    step_fn()
+    alt_fn()
     torch.cuda.synchronize()
     eta_alt = sweep.eta.clone()
     if sweep.record == "jumps":

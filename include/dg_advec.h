@@ -150,13 +150,23 @@ int dg_plan_query(const dg_plan* plan, int64_t out[8]);
  *                             Bit-identical results
  *   DG_TUNE_P_SWEEP           dg_lserk4_sweep_p: 1 (default) runs the snapshot forward and the
  *                             estimate as ONE dataflow launch where dg_plan_query_p_sweep
- *                             allows; 0 the chains.  Bit-identical results
+ *                             allows; 0 the chains, whose forward runs at 4 steps per launch
+ *                             like the launch's blocks.  Bit-identical results (a separate
+ *                             dg_lserk4_fwd at another steps per launch rounds differently)
+ *   DG_TUNE_NL_EXCHANGE       the config-3 kernels (nonlinear flux and/or per-stage limiter,
+ *                             dg_lserk4_fwd(_ex) / dg_lserk4_adj(_ex)): 0 workgroup tiles
+ *                             exchanging faces and cell averages through LDS with a barrier
+ *                             each; 1 overlapped waves: every wave owns 44 of a 64-element
+ *                             window, every exchange a DPP wave shift, no barrier inside a step
+ *                             (one step per forward launch; the limited adjoint needs the
+ *                             decision record, else it runs the workgroup tiles).
+ *                             Bit-identical results
  *   DG_TUNE_SWEEP_SPIN_LIMIT  diagnostics/tests: polls a dataflow work item makes before it
  *                             gives up waiting for a producer (0: the default, ~2^20; 1 makes
  *                             the watchdog fire on any multi-block sweep)
  * Environment overrides at plan creation: DG_TILE_WIDTH, DG_STEPS_PER_LAUNCH, DG_LANE_ELEMENTS,
  * DG_REC_TILE_WIDTH, DG_REC_FWD_TILE_WIDTH, DG_REC_STEPS_PER_LAUNCH, DG_REC_FWD_STEPS_PER_LAUNCH, DG_REC_LANE_ELEMENTS,
- * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE, DG_SNAP_PAIRS, DG_P_FLOW, DG_P_SWEEP. */
+ * DG_P_TILE_WIDTH, DG_P_STEPS_PER_LAUNCH, DG_SWEEP_WAVES, DG_SWEEP_LANE_ELEMENTS, DG_SWEEP_EXCHANGE, DG_SNAP_PAIRS, DG_P_FLOW, DG_P_SWEEP, DG_NL_EXCHANGE. */
 enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER = 3,
        DG_TUNE_LANE_ELEMENTS = 4, DG_TUNE_REC_TILE_WIDTH = 5, DG_TUNE_REC_STEPS_PER_LAUNCH = 6,
        DG_TUNE_REC_LANE_ELEMENTS = 7, DG_TUNE_REC_FWD_STEPS_PER_LAUNCH = 8,
@@ -164,7 +174,8 @@ enum { DG_TUNE_TILE_WIDTH = 1, DG_TUNE_STEPS_PER_LAUNCH = 2, DG_TUNE_XCD_ORDER =
        DG_TUNE_REC_FWD_TILE_WIDTH = 11, DG_TUNE_REC_SWEEP = 12,
        DG_TUNE_SWEEP_SPIN_LIMIT = 13, DG_TUNE_SWEEP_WAVES = 14,
        DG_TUNE_SWEEP_LANE_ELEMENTS = 15, DG_TUNE_SWEEP_TAKE = 16, DG_TUNE_SWEEP_EXCHANGE = 17,
-       DG_TUNE_SNAP_PAIRS = 18, DG_TUNE_P_FLOW = 19, DG_TUNE_P_SWEEP = 20 };
+       DG_TUNE_SNAP_PAIRS = 18, DG_TUNE_P_FLOW = 19, DG_TUNE_P_SWEEP = 20,
+       DG_TUNE_NL_EXCHANGE = 21 };
 int dg_plan_tune(dg_plan* plan, int key, int64_t value);
 
 /* The jump-record sweeps' effective shape: out[0] = tile width, out[1] = steps per launch
@@ -339,10 +350,17 @@ int dg_plan_query_sweep_kernel(const dg_plan* plan, int nsteps, int64_t out[8]);
  * later dg_lserk4_sweep_rec / dg_lserk4_sweep_refine call of the plan returns DG_ERR_HIP
  * (without a device sync) until dg_sweep_status clears it. */
 int dg_sweep_status(dg_plan* plan, int* status, void* stream);
-/* Profiling: with trace non-null (device, 4 uint64 per work item, dg_plan_query_sweep's
- * out[3] items), every later dataflow sweep of the plan records per item the wall-clock
- * (100 MHz) times it was taken and its producers were done and it was published, and
- * (XCC id << 32 | workgroup id).  NULL turns it off. */
+/* Profiling: with trace non-null (device), every later dataflow launch of the plan records
+ * per work item the wall-clock (100 MHz) times it was taken and its producers were done and
+ * it was published, and (XCC id << 32 | workgroup id): 4 uint64 per item of the jump sweep
+ * (dg_plan_query_sweep's out[3] items), 8 per item of the p launches (dg_lserk4_adj_p /
+ * dg_lserk4_sweep_p: dg_plan_query_p_trace).  Size it for every launch the plan runs while
+ * the trace is on.  NULL turns it off.
+ * HIP graphs: the dataflow launches share the plan's control words (take counter, epochs),
+ * kept across launches of one shape; a dataflow call of another shape (kind, nsteps, tile,
+ * waves, steps per block) re-zeroes them.  A graph that captured a dataflow launch stays
+ * valid only while no call of another shape runs on the plan between its replays: re-capture
+ * after one. */
 int dg_plan_sweep_trace(dg_plan* plan, uint64_t* trace);
 
 /* ---------------------------------------------------------------------------------------
@@ -399,8 +417,9 @@ int dg_plan_query_p_flow(const dg_plan* lo, int nsteps, int* out);
  * dg_lserk4_adj_p_refine.  Where the shape allows (dg_plan_query_p_sweep: the dataflow
  * estimate at 4-step blocks, the forward's workgroup tiles, 2..8 blocks) both directions run
  * as ONE dataflow launch (k_psweep: forward blocks then estimate blocks as work items), else
- * as dg_lserk4_fwd_ex + dg_lserk4_adj_p(_refine).  Bit-identical to dg_lserk4_fwd_ex with
- * the lo plan's steps per launch at 4 followed by dg_lserk4_adj_p.  flags: DG_ADJ_ETA_ASSIGN /
+ * as dg_lserk4_fwd_ex at 4 steps per launch on the stage-loop workgroup tiles (whatever the
+ * plan's steps per launch) + dg_lserk4_adj_p(_refine): the same bits either way, and the same
+ * as dg_lserk4_fwd_ex with the lo plan's steps per launch at 4 followed by dg_lserk4_adj_p.  flags: DG_ADJ_ETA_ASSIGN /
  * _ABS.  Replaces the reference's forward march + adjoint march + error estimate
  * (matlab/MAIN.m:32-34, adj_march.m:103-117). */
 int dg_lserk4_sweep_p(dg_plan* lo, dg_plan* hi, const double* P, double* snapshots, double* w,
@@ -409,6 +428,13 @@ int dg_lserk4_sweep_p(dg_plan* lo, dg_plan* hi, const double* P, double* snapsho
 
 /* *out = 1 if dg_lserk4_sweep_p over nsteps steps runs as one dataflow launch, else 0. */
 int dg_plan_query_p_sweep(const dg_plan* lo, int nsteps, int* out);
+
+/* The p launches' trace records (dg_plan_sweep_trace): out[0] = work items of
+ * dg_lserk4_adj_p's dataflow launch over nsteps (0: it runs as a launch chain), out[1] = work
+ * items of dg_lserk4_sweep_p's (0: the chains), out[2] = uint64 words each item writes (8).  A
+ * trace buffer on a plan that runs these launches needs out[2] * max(out[0], out[1]) words
+ * besides the jump sweep's 4 * dg_plan_query_sweep out[3]. */
+int dg_plan_query_p_trace(const dg_plan* lo, int nsteps, int64_t out[3]);
 
 /* ulim = SlopeLimitN(u)  — utils/SlopeLimitN.m:1-33 with SlopeLimitLin.m:1-19 and minmod.m:1-13.
  * ids_mask (nullable): per element 1 if limited (the `ids` of SlopeLimitN.m:23), else 0. */

@@ -419,3 +419,113 @@ def test_full_size_config3_adjoint_and_indicator(pkg, gpu):
   _, ids = ob.limited_step(u_mid, times[1], dt, A, window_setup(N, v_x, k_jump, k_jump + 400,
                                                                   s_glob), return_ids=True)
   assert sum(i.size for i in ids) > 0
+
+
+def _device_ic(pkg, run, gpu, seed=7):
+  """u0 = sin(2 pi x) + 0.8 (x > 0.5) + seeded per-node noise on the run's current mesh,
+  built on the device from the node coordinates (the noise keeps every interelement jump
+  O(0.01): a smooth IC's jumps at h = 2^-22 are below fp64 resolution)."""
+  import torch
+  N = run.op.N
+  r = torch.tensor(setup1d.jacobi_gl(0, 0, N), dtype=torch.float64, device=gpu)
+  vx = torch.tensor(run.op.v_x(), dtype=torch.float64, device=gpu)
+  xd = vx[:-1, None] + 0.5 * (r[None, :] + 1.0) * (vx[1:] - vx[:-1])[:, None]
+  gen = torch.Generator(device=gpu).manual_seed(seed)
+  noise = torch.randn(xd.shape, generator=gen, dtype=torch.float64, device=gpu)
+  return (torch.sin(2 * np.pi * xd) + 0.8 * (xd > 0.5) + 0.01 * noise).reshape(-1)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("exchange", [1, 0])
+def test_full_size_config3_bench_path(pkg, gpu, exchange):
+  """The timed config-3 instantiation against the oracle: BASELINE config
+  3's N = 4, K = 2^22 through adaptive.AdaptiveSweep -- the bench's own calls, forward with the
+  decision record and the adjoint in place on u^N reading it -- after device refinements (two
+  adapt iterations, then splits placed inside the checked windows), so the plan is non-uniform
+  and the UNI = false kernels run; 20 + 20 steps; a jump IC, so troubled cells exist every step
+  and the adjoint's wide-cone pass runs beside the narrow-cone tiles / windows (the decision
+  record is checked to hold troubled cells).  Both exchanges (DG_TUNE_NL_EXCHANGE).
+
+  The oracle (oracle/burgers.py) runs on windows of the refined mesh: an output depends only on
+  its cone -- 10 elements per limited step and side for the forward, and for w^0 / eta 10 per
+  reverse step on the GPU's own snapshots -- so 220 elements in from a cut the windowed oracle
+  is the full-size oracle after 20 steps.  Windows: the inflow boundary, the jump at x = 0.5
+  (troubled cells, refined elements), a random interior stretch with refined elements, the
+  outflow boundary, and the GPU's top-2 |eta| elements.  Forward states: every snapshot within
+  1e-10 of max|oracle|; w^0 and eta likewise.  The refine index: the device argmax is numpy's
+  argmax of the GPU's |eta|, and when its margin over the runner-up clears the parity
+  tolerance, the oracle ranks the two the same way."""
+  import torch
+  N, K0, nsteps, margin, width = 4, 1 << 22, 20, 220, 800
+  Np = N + 1
+  mesh = pkg.BaseGalerkin1D(n=N, k=K0, domain=[0.0, 1.0])
+  run = pkg.adaptive.AdaptiveSweep(mesh, nsteps, 16, flux="burgers", limiter=True)
+  run.op.tune(nl_exchange=exchange)
+  for _ in range(2):  # the bench's iterations (sin IC): argmax |eta| and the device split
+    run.iterate()
+  rng = np.random.default_rng(2026)
+  k_jump = int(np.searchsorted(run.op.v_x(), 0.5))
+  k_rand = int(rng.integers(20000, K0 - 20000))
+  for j in (k_jump - 120, k_jump + 90, k_rand + 300, k_rand + 301, k_rand + 500):
+    run.op.refine(torch.tensor([j], dtype=torch.int64, device=gpu))
+  run.h_min = float(np.min(np.diff(run.op.v_x())))  # the CFL step on the refined mesh
+  assert not run.op.uniform
+  v_x = run.op.v_x()
+  K = run.K
+  snaps = run.snapshots()
+  snaps[0].copy_(_device_ic(pkg, run, gpu))
+  dt = run.dt
+  run.forward(dt, init=False)
+  uN = snaps[nsteps].clone()  # the terminal weight: the adjoint runs in place on u^N
+  run.adjoint(dt)
+  eta = run.eta()
+  idx = run.op.argmax(eta, use_abs=True)
+  torch.cuda.synchronize()
+  dec = run.decisions()
+  assert int(torch.count_nonzero(dec)) > 0  # troubled cells: the wide pass ran
+  top = torch.topk(eta.abs(), 2)
+  i1, i2 = (int(i) for i in top.indices)
+  assert idx == i1 == int(np.argmax(np.abs(host(eta))))
+  times = [0.0]
+  for _ in range(nsteps):
+    times.append(times[-1] + dt)
+  k_jump = int(np.searchsorted(v_x, 0.5))
+  windows = [(0, width), (k_jump - width // 2, k_jump + width // 2),
+             (k_rand, k_rand + width), (K - width, K)]
+  for c in (i1, i2):
+    k0 = min(max(c - width // 2, 0), K - width)
+    windows.append((k0, k0 + width))
+  h = np.diff(v_x)
+  refined = np.flatnonzero(h < h.max() * 0.75)
+  eta_ref_at = {}
+  for k0, k1 in windows:
+    S = setup1d.startup1d(N, v_x[k0:k1 + 1] - v_x[k0], metric="element")
+    sl = slice(k0 * Np, k1 * Np)
+    lo = 0 if k0 == 0 else margin  # a real boundary needs no margin
+    hi = (k1 - k0) if k1 == K else (k1 - k0) - margin
+    gs = [setup1d.from_elem_major(host(snaps[n][sl]), Np) for n in range(nsteps)]
+    gs.append(setup1d.from_elem_major(host(uN[sl]), Np))
+    ref, _ = ob.forward_sweep(gs[0], 0.0, dt, nsteps, A, S)
+    for n in range(1, nsteps + 1):
+      err = rel_err(gs[n][:, lo:hi], ref[n][:, lo:hi])
+      assert err <= RTOL, (k0, n, err)
+    w_ref, eta_ref, _ = ob.adjoint_sweep(gs[-1], gs, times, dt, A, S, limit=True)
+    got_w = setup1d.from_elem_major(host(snaps[nsteps][sl]), Np)[:, lo:hi]
+    assert rel_err(got_w, w_ref[:, lo:hi]) <= RTOL, (k0, rel_err(got_w, w_ref[:, lo:hi]))
+    got_eta = host(eta[k0:k1])[lo:hi]
+    assert rel_err(got_eta, eta_ref[lo:hi]) <= RTOL, (k0, rel_err(got_eta, eta_ref[lo:hi]))
+    for c in (i1, i2):
+      if k0 + lo <= c < k0 + hi:
+        eta_ref_at[c] = abs(float(eta_ref[c - k0]))
+  # refined elements were inside checked windows
+  inside = [k for k in refined for k0, k1 in windows[1:3] if k0 + margin <= k < k1 - margin]
+  assert len(inside) >= 3, inside
+  # the refine decision: the oracle's |eta| at the GPU's top two, ranked the same way when the
+  # GPU's margin clears the tolerance (1e-10 of the top value, twice: both values may move)
+  assert i1 in eta_ref_at and i2 in eta_ref_at
+  v1, v2 = float(top.values[0]), float(top.values[1])
+  if v1 - v2 > 2 * RTOL * v1:
+    assert eta_ref_at[i1] > eta_ref_at[i2]
+  run.refine()
+  assert run.sync() == i1
+  np.testing.assert_array_equal(run.op.v_x(), pkg.split_interval(v_x, i1))

@@ -178,3 +178,43 @@ def test_psweep_full_size(pkg, gpu):
   op, est, u0, dt = setup(pkg, gpu, 4, 1 << 20, 1, seed=21)
   assert_same(fused(op, est, u0, dt, 20), chain(op, est, u0, dt, 20), "full size")
   assert op.sweep_status() == 0
+
+
+def test_psweep_fallback_ignores_the_plans_steps_per_launch(pkg, gpu):
+  """The chains dg_lserk4_sweep_p falls back to run the forward at the dataflow launch's 4-step
+  blocks whatever the lo plan's steps per launch: a sweep whose nsteps does not
+  fit the launch (36 > 32 steps, 6 = not 4-step blocks) and one that does give the bits of the
+  4-step chain even with the plan tuned to 8 (or 2) steps per launch."""
+  op, est, u0, dt = setup(pkg, gpu, 4, 1200, 1, seed=9)
+  refs = {n: chain(op, est, u0, dt, n) for n in (36, 6, 12)}  # chain: op at 4 steps per launch
+  for spl in (8, 2):
+    op.tune(tile_width=2, steps_per_launch=spl)
+    for n, fits in ((36, False), (6, False), (12, True)):
+      assert est.query_sweep(n) == fits
+      assert_same(fused(op, est, u0, dt, n), refs[n], (spl, n))
+  op.tune(steps_per_launch=4)
+
+
+def test_p_trace_buffer_is_sized_by_the_query(pkg, gpu):
+  """dg_plan_query_p_trace gives the p launches' trace size (8 words per work item; ADVICE
+  r05): a trace of exactly that many words, followed by a canary, is filled by the estimate's
+  and the sweep's dataflow launches and the canary is untouched."""
+  import torch
+  op, est, u0, dt = setup(pkg, gpu, 4, 5000, 1, seed=10)
+  nsteps = 20
+  assert est.query_flow(nsteps) and est.query_sweep(nsteps)
+  words = est.trace_words(nsteps)
+  tiles = -(-op.ktot // (256 * 2 - 40))  # the 4-step blocks' 512-element tiles
+  assert words == 8 * 2 * (nsteps // 4) * tiles  # the sweep's launch: forward + estimate items
+  canary = 1 << 62
+  buf = torch.full((words + 64,), canary, dtype=torch.int64, device=gpu)
+  op.sweep_trace(buf[:words])
+  try:
+    fused(op, est, u0, dt, nsteps)
+    chain(op, est, u0, dt, nsteps)  # the estimate's own dataflow launch
+  finally:
+    op.sweep_trace(None)
+  torch.cuda.synchronize()
+  tr = host(buf)
+  assert (tr[words:] == canary).all()
+  assert (tr[:words] != canary).all()  # every item recorded (the sweep's launch fills all)
