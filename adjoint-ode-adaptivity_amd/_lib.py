@@ -68,6 +68,7 @@ SIGNATURES = {
                                 _vp]),
     "dg_plan_query_rec": (_i32, [_vp, _vp]),
     "dg_plan_query_rec_fwd": (_i32, [_vp, _vp]),
+    "dg_plan_query_nl": (_i32, [_vp, _vp]),
     "dg_lserk4_fwd_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,
                                  _vp]),
     "dg_lserk4_adj_rec": (_i32, [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _i32, _vp,

@@ -1329,6 +1329,11 @@ int dg_plan_query_rec_fwd(const dg_plan* p, int64_t out[2]) {
   return DG_OK;
 }
 
+int dg_plan_query_nl(const dg_plan* p, int64_t out[3]) {
+  if (!p || !out) return fail(DG_ERR_ARG, "null argument");
+  return nl_query(p, out);
+}
+
 int dg_plan_query_p(const dg_plan* p, int64_t out[2]) {
   if (!p || !out) return fail(DG_ERR_ARG, "null argument");
   out[0] = p->p_tile_width;

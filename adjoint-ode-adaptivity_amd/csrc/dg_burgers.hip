@@ -503,6 +503,13 @@ inline int chunk_nl(const dg_plan* p, int left, bool snapshots) {
 
 namespace dgk {
 
+int nl_query(const dg_plan* p, int64_t out[3]) {
+  out[0] = p->nl_exchange;
+  out[1] = chunk_nl(p, 1 << 30, true);
+  out[2] = chunk_nl(p, 1 << 30, false);
+  return DG_OK;
+}
+
 int nl_rhs(const dg_plan* p, const double* u, double* rhs, double t, hipStream_t st) {
   const double fin = flux_value(true, inflow_value(p, t));
   const unsigned grid = grid_for(p->ktot, kBlock);

@@ -631,6 +631,7 @@ inline unsigned grid_for(int64_t n, int64_t per) { return unsigned((n + per - 1)
 // Nonlinear-flux / per-stage-limiter steppers (dg_burgers.hip), dispatched from the C ABI
 // when plan->nonlinear().
 int nl_rhs(const dg_plan* p, const double* u, double* rhs, double t, hipStream_t st);
+int nl_query(const dg_plan* p, int64_t out[3]);  // dg_plan_query_nl
 int nl_fwd(dg_plan* p, double* u, double t0, double dt, int nsteps, double* snapshots,
            uint16_t* decisions, hipStream_t st);
 int nl_adj(dg_plan* p, double* w, const double* snapshots, double t0, double dt, int nsteps,

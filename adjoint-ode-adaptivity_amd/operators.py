@@ -115,6 +115,12 @@ class DGAdvection1D:
     f = (ctypes.c_int64 * 2)()
     _lib.check(self._lib.dg_plan_query_rec_fwd(self._plan, f), "dg_plan_query_rec_fwd")
     self.rec_fwd_tile_width = int(f[0])
+    n = (ctypes.c_int64 * 3)()
+    _lib.check(self._lib.dg_plan_query_nl(self._plan, n), "dg_plan_query_nl")
+    # the config-3 kernels: exchange (0 workgroup tiles, 1 overlapped waves), forward steps
+    # per launch with / without snapshots
+    self.nl_exchange = int(n[0])
+    self.nl_steps_per_launch = (int(n[1]), int(n[2]))
 
   # --- lifetime ---
   def close(self):

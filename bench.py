@@ -472,8 +472,12 @@ def main_config3(args, world, rank, dev):
   total = sum_over_ranks(total, world, dev, args.backend)
   Np = N + 1
   k_mid = K + warm + args.steps // 2
-  # forward steps per launch with snapshots (dg_burgers.hip chunk_nl): 2 only when tuned to 2
-  ms = 2 if run.op.steps_per_launch == 2 else 1
+  # forward steps per launch with snapshots (dg_burgers.hip chunk_nl): 2 only when tuned to 2;
+  # the exchange: workgroup tiles (k_step_nl / k_adj_nl + k_adj_nl_wide) or overlapped waves
+  # (k_step_nlw / k_adj_nlw + k_adj_nlw_wide, DG_TUNE_NL_EXCHANGE)
+  ms = run.op.nl_steps_per_launch[0]
+  ow = run.op.nl_exchange == 1
+  kf_name, ka_name = ("k_step_nlw", "k_adj_nlw") if ow else ("k_step_nl", "k_adj_nl")
   fwd_launches = (nsteps + ms - 1) // ms
   fwd_us = [e[0].elapsed_time(e[1]) * 1e3 / fwd_launches for e in evs]
   adj_us = [e[2].elapsed_time(e[3]) * 1e3 / nsteps for e in evs]
@@ -504,15 +508,21 @@ def main_config3(args, world, rank, dev):
       "roofline": {"bound": "hbm", "achieved": adj_bytes / (adj_m * 1e-6) / 1e9,
                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
                    "frac": adj_bytes / (adj_m * 1e-6) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                   "kernel": f"k_adj_nl<{Np},burgers,limiter,nonuniform> (1 reverse step + "
-                             f"stage recompute + DWR per launch, tiles on the narrow cone; "
-                             f"+ k_adj_nl_wide for tiles with a troubled cell)",
+                   "kernel": (f"k_adj_nlw<{Np},burgers,limiter,nonuniform> (1 reverse step + "
+                              f"stage recompute + DWR per launch on overlapped-wave windows, "
+                              f"narrow cone; + k_adj_nlw_wide for windows with a troubled cell)"
+                              if ow else
+                              f"k_adj_nl<{Np},burgers,limiter,nonuniform> (1 reverse step + "
+                              f"stage recompute + DWR per launch, tiles on the narrow cone; "
+                              f"+ k_adj_nl_wide for tiles with a troubled cell)"),
+                   "exchange": "overlapped waves (DPP)" if ow else "workgroup tiles (LDS)",
                    "launch_us": adj_m, "launch_us_stats": stats(adj_us),
                    "algorithmic_bytes": adj_bytes},
       "roofline_fwd": {"bound": "hbm", "achieved": fwd_bytes / (fwd_m * 1e-6) / 1e9,
                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": fwd_bytes / (fwd_m * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                       "kernel": f"k_step_nl<{Np},burgers,limiter,nonuniform,{ms}>",
+                       "kernel": (f"k_step_nlw<{Np},burgers,limiter,nonuniform>" if ow else
+                                  f"k_step_nl<{Np},burgers,limiter,nonuniform,{ms}>"),
                        "launch_us": fwd_m, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
       "refine_index": ref_idx,
@@ -524,21 +534,22 @@ def main_config3(args, world, rank, dev):
   # per launch, and the issued fp64 rate = the profile's issued flops per launch / this run's
   # launch time (every lane of a wave counted: halo lanes included).
   try:
-    with open(os.path.join(ROOT, "profiles", "r05", "config3", "pmc.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r06", "config3", "pmc.json")) as f:
       prof = json.load(f)
   except (OSError, ValueError):
     prof = None
   if prof and prof.get("N") == N and prof.get("K") == K:
     uni = "false"  # after its first split the refine loop's mesh is non-uniform
     pk = {k: v for k, v in prof["kernels"].items() if f", {uni}," in k or k.endswith(f", {uni}>")}
-    ka = next((v for k, v in pk.items() if k.startswith("k_adj_nl<")), None)
-    kw = next((v for k, v in pk.items() if k.startswith("k_adj_nl_wide<")), None)
+    ka = next((v for k, v in pk.items() if k.startswith(ka_name + "<")), None)
+    kw = next((v for k, v in pk.items() if k.startswith(ka_name + "_wide<")), None)
     if ka and kw:  # one wide-cone pass per reverse step: count its bytes and flops with it
       ka = dict(ka)
       for key in ("hbm_bytes_per_launch", "fp64_flops_issued_per_launch"):
         if key in ka and key in kw:
           ka[key] += kw[key]
-    kf = next((v for k, v in pk.items() if k.startswith("k_step_nl") and k.endswith(f", {ms}>")), None)
+    kf = next((v for k, v in pk.items() if k.startswith(kf_name + "<")
+               and (ow or k.endswith(f", {ms}>"))), None)
     src = prof.get("source")
     if ka and "hbm_bytes_per_launch" in ka:
       out["roofline"].update({"traffic": ka["hbm_bytes_per_launch"], "traffic_from_profile": True,
@@ -927,10 +938,12 @@ def main(argv=None):
       snap_adj += snap_fwd
     eff_adj = snap_adj / (adj_launch_us * 1e-6) / 1e9
     eff_fwd = snap_fwd / (fwd_launch_us * 1e-6) / 1e9
-    effective = {"what": "launch times priced with the snapshot sweep's algorithmic bytes for "
-                         "the same steps (effective, not moved)",
-                 "adj_GBs": eff_adj, "adj_frac": eff_adj / HBM_PEAK_GBS,
-                 "fwd_GBs": eff_fwd, "fwd_frac": eff_fwd / HBM_PEAK_GBS}
+    effective = {"what": "NOT moved bandwidth: the launch times priced with the bytes the "
+                         "snapshot sweep would move for the same steps (what storing 8 B per "
+                         "element-step instead of a snapshot saves); moved bytes are "
+                         "roofline_hbm's algorithmic_bytes and traffic",
+                 "adj_GBs_equiv": eff_adj, "adj_frac_equiv": eff_adj / HBM_PEAK_GBS,
+                 "fwd_GBs_equiv": eff_fwd, "fwd_frac_equiv": eff_fwd / HBM_PEAK_GBS}
   total_dofs = sum_over_ranks(sweep.dof_updates, world, dev, args.backend) * args.steps
   value = total_dofs / elapsed
   # The single-step algorithm moves 16 B (fwd) + 24 B + 16/Np B (adj) per pair of
@@ -1000,7 +1013,7 @@ def main(argv=None):
                        "kernel": f"{kstep}<{Np},uniform,{tile_tag_fwd},{fms}{rec_tag}> ({fms} steps per launch)",
                        "launch_us": fwd_launch_us, "launch_us_stats": stats(fwd_us),
                        "algorithmic_bytes": fwd_bytes},
-      "roofline_effective": effective,
+      "snapshot_bytes_equivalent": effective,
       # The compute roof of the same launches: the even/odd algorithm's fp64 flops (interior
       # elements) / launch time, against the spec and the on-box FMA probe; issued_frac
       # counts the halo lanes each tile also computes (the work the lanes actually issue).
@@ -1117,8 +1130,8 @@ def main(argv=None):
                  "launch time (adj_*: the one dataflow launch); adj_issued_frac weights each "
                  "direction's issued/useful lanes (halo) by its flops")
     out["stream_copy"]["fwd_frac_of_achievable"] = None
-    if out.get("roofline_effective"):
-      out["roofline_effective"].update({"fwd_GBs": None, "fwd_frac": None})
+    if out.get("snapshot_bytes_equivalent"):
+      out["snapshot_bytes_equivalent"].update({"fwd_GBs_equiv": None, "fwd_frac_equiv": None})
     # the PMC-measured issued fp64 flops of the same launch (SQ passes of this bench,
     # profiles/r04/collect.sh), from the profile whose traffic matched
     try:
@@ -1133,6 +1146,20 @@ def main(argv=None):
         f["pmc_source"] = os.path.relpath(os.path.join(prof_dir, "sq_summary.json"), ROOT)
     except (OSError, ValueError, KeyError, TypeError):
       pass
+    # The launch's binding roof is fp64 issue (8 B per element-step of record: HBM is far
+    # from bound): `roofline` carries it, the HBM view sits beside it.
+    hbm = out.pop("roofline")
+    out["roofline"] = {
+        "bound": "fp64 vector", "achieved": f["adj_achieved"], "peak": FP64_PEAK_TFLOPS,
+        "unit": "TFLOP/s", "frac": f["adj_achieved"] / FP64_PEAK_TFLOPS,
+        "issued_frac": f["adj_issued_frac"], "pmc_issued_frac": f.get("pmc_issued_frac"),
+        "traffic": hbm["traffic"], "traffic_unit": "HBM bytes per launch (PMC FETCH+WRITE)",
+        "hbm_frac": hbm["frac"], "kernel": hbm["kernel"], "launch_us": hbm["launch_us"],
+        "launch_us_stats": hbm["launch_us_stats"],
+        "what": ("useful fp64 flops of both directions' interior elements per launch / launch "
+                 "time (achieved, frac); issued_frac adds the halo lanes, pmc_issued_frac is "
+                 "the PMC count; the HBM view (algorithmic bytes, traffic) is roofline_hbm")}
+    out["roofline_hbm"] = hbm
     out["dataflow"] = {"launches_per_sweep": 1, "blocks_fwd": fchunks, "blocks_adj": chunks,
                        "refine_in_launch": fused_refine,
                        "refine_to_host": "written by the launch into pinned memory (dg_host_alias)"

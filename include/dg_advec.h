@@ -188,6 +188,11 @@ int dg_plan_query_rec_fwd(const dg_plan* plan, int64_t out[2]);
 /* The p-enriched estimate's effective shape: out[0] = tile width, out[1] = steps per launch. */
 int dg_plan_query_p(const dg_plan* plan, int64_t out[2]);
 
+/* The config-3 kernels' shape (nonlinear flux and/or limiter): out[0] = the exchange
+ * (DG_TUNE_NL_EXCHANGE: 0 workgroup tiles, 1 overlapped waves), out[1] = forward steps per
+ * launch with snapshots, out[2] = without. */
+int dg_plan_query_nl(const dg_plan* plan, int64_t out[3]);
+
 /* Physics of the plan's steppers.  Default: DG_FLUX_LINEAR + DG_LIMIT_NONE (AdvecRHS1D).
  *   DG_FLUX_LINEAR      f(u) = a*u                               utils/AdvecRHS1D.m:9-19
  *   DG_FLUX_BURGERS     f(u) = a*u^2/2 at the nodes with AdvecRHS1D's central-flux structure

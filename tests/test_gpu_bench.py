@@ -34,7 +34,13 @@ def test_bench_single_rank_line(gpu, dataflow):
               "--no-cpu-baseline"], env_extra={"DG_REC_SWEEP": "1" if dataflow else "0"})
   assert out["n_gpus"] == 1 and out["steps"] == 3 and out["warmup_effective"] == 2
   assert out["unit"] == "DOF-updates/s" and out["value"] > 0
-  assert out["roofline"]["bound"] == "hbm" and 0 < out["roofline"]["frac"] < 1
+  # the dataflow sweep's binding roof is fp64 issue, the chains' HBM
+  assert out["roofline"]["bound"] == ("fp64 vector" if dataflow else "hbm")
+  assert 0 < out["roofline"]["frac"] < 1
+  if dataflow:
+    assert out["roofline_hbm"]["bound"] == "hbm" and 0 < out["roofline_hbm"]["frac"] < 1
+    assert out["roofline"]["frac"] == out["roofline_fp64"]["adj_frac"]
+  assert "roofline_effective" not in out
   assert out["nonfinite_indicator_steps"] == 0
   assert out["stream_copy"]["achievable_GBs"] > 1000
   assert out["refine_index_ranks"] == [out["refine_index"]]
