@@ -95,6 +95,23 @@ __device__ __forceinline__ void flux_eo(const double* ev, const double* od, doub
   if constexpr (NE > NO) fe[NO] = BURG ? (HQ ? ev[NO] * ev[NO] : 0.5 * ev[NO] * ev[NO]) : ev[NO];
 }
 
+// An element's face fluxes f(u_0) = fe_0 + fo_0, f(u_N) = fe_0 - fo_0 (HQ: fe_0 doubled).
+// Burgers' fo_0 = e o is a bare product, and fe_0 + e o may be contracted into fma(e, o, fe_0)
+// -- or not, depending on the code around it: the two exchange layouts would then round the
+// same face differently.  The product is materialised first (pin), so the face is always the
+// rounded sum of the rounded product, which is also what HQ's fma(0.5, 2 fe_0, fo_0) gives.
+template <bool BURG, bool HQ>
+__device__ __forceinline__ void face_values(double fe0, double fo0, double& f0, double& fN) {
+  if constexpr (HQ) {
+    f0 = fma(0.5, fe0, fo0);
+    fN = fma(0.5, fe0, -fo0);
+  } else {
+    if constexpr (BURG) pin(fo0);
+    f0 = fe0 + fo0;
+    fN = fe0 - fo0;
+  }
+}
+
 // Exchange arrays in LDS (doubles, each padded by one slot on the left): two
 // double-buffered face pairs [0, 4(T+2)), cell averages [4(T+2), 5(T+2)), the adjoint's
 // limiter contributions to the left / right neighbour [5(T+2), 7(T+2)), the indicator's
@@ -284,8 +301,8 @@ __device__ __forceinline__ int nl_stage(X& x, int s, int par, int iin, double fi
   // limiter no barrier separates a step's last face reads from the next step's writes)
   double fe[NE], fo[NO];
   flux_eo<NP, BURG, HQ>(ev, od, fe, fo);
-  const double f0 = HQ ? fma(0.5, fe[0], fo[0]) : fe[0] + fo[0];
-  const double fN = HQ ? fma(0.5, fe[0], -fo[0]) : fe[0] - fo[0];
+  double f0, fN;
+  face_values<BURG, HQ>(fe[0], fo[0], f0, fN);
   x.face_put(par, f0, fN);
   __builtin_amdgcn_sched_barrier(0);
   double pe[NE], po[NO];  // volume term + the carry A_s r'
@@ -465,8 +482,7 @@ __device__ __forceinline__ double nl_adj_body(X& x, const Elem& E, double sc, in
   if (args.has_eta) {
     double fe[NE], fo[NO];
     flux_eo<NP, BURG>(ev, od, fe, fo);
-    uf0 = fe[0] + fo[0];
-    ufN = fe[0] - fo[0];
+    face_values<BURG, false>(fe[0], fo[0], uf0, ufN);
 #pragma unroll
     for (int k = 0; k < NE; ++k) ipe = fma(args.op.le[k], we[k], ipe);
 #pragma unroll

@@ -11,7 +11,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -- python3 "$B" --config 3 --steps 2 --warmup 1 --no-converge --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1 || { echo "pmc fetch failed"; tail -5 "$OUT/pmc_fetch.log"; exit 1; }
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -- python3 "$B" --config 3 --steps 2 --warmup 1 --no-converge --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1 || { echo "pmc write failed"; tail -5 "$OUT/pmc_write.log"; exit 1; }
 timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_WAVES --output-format csv -d "$OUT/pmc_sq" -- python3 "$B" --config 3 --steps 2 --warmup 1 --no-converge --no-cpu-baseline > "$OUT/pmc_sq.log" 2>&1 || { echo "pmc sq failed"; tail -5 "$OUT/pmc_sq.log"; exit 1; }
-timeout -s KILL 150 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU --output-format csv -d "$OUT/pmc_wait" -- python3 "$B" --config 3 --steps 2 --warmup 1 --no-converge --no-cpu-baseline > "$OUT/pmc_wait.log" 2>&1 || { echo "pmc wait failed"; tail -5 "$OUT/pmc_wait.log"; }
+timeout -s KILL 150 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES --output-format csv -d "$OUT/pmc_wait" -- python3 "$B" --config 3 --steps 2 --warmup 1 --no-converge --no-cpu-baseline > "$OUT/pmc_wait.log" 2>&1 || { echo "pmc wait failed"; tail -5 "$OUT/pmc_wait.log"; }
 STATS=$(find "$OUT/prof" -name '*kernel_stats.csv' -print -quit); cp "$STATS" "$OUT/kernel_stats.csv"
 FETCH=$(find "$OUT/pmc_fetch" -name '*counter_collection.csv' -print -quit)
 WRITE=$(find "$OUT/pmc_write" -name '*counter_collection.csv' -print -quit)

@@ -52,6 +52,8 @@ def main():
                                                   "SQ_INSTS_VALU_MUL_F64"))
   wait, cyc, valu = (per_kernel(a.wait, c) for c in ("SQ_WAIT_ANY", "SQ_WAVE_CYCLES",
                                                       "SQ_ACTIVE_INST_VALU"))
+  ivalu, isalu, ilds, waves = (per_kernel(a.wait, c) for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU",
+                                                               "SQ_INSTS_LDS", "SQ_WAVES"))
   for k in stats:
     if not re.match(r"k_(step|adj)_nl", k):
       continue
@@ -64,6 +66,13 @@ def main():
     if cyc.get(k) and mean(cyc[k]) > 0:
       d["wait_any_frac"] = mean(wait.get(k, [])) / mean(cyc[k])
       d["valu_active_frac"] = mean(valu.get(k, [])) / mean(cyc[k])
+    if ivalu.get(k) and waves.get(k) and mean(waves[k]) > 0:
+      # VALU / SALU / LDS instructions per wave, and all of a launch's VALU instructions
+      w = mean(waves[k])
+      d["valu_insts_per_wave"] = mean(ivalu[k]) / w
+      d["salu_insts_per_wave"] = mean(isalu.get(k, [])) / w
+      d["lds_insts_per_wave"] = mean(ilds.get(k, [])) / w
+      d["valu_insts_per_launch"] = mean(ivalu[k])
     out["kernels"][k] = d
   json.dump(out, open(a.out, "w"), indent=1)
   print(json.dumps(out, indent=1))
