@@ -54,7 +54,10 @@ __device__ __forceinline__ void put_interior(double* __restrict__ lds, const dou
 // elements.  Measured at K = 2^22 (bench.py --config 3): the forward (64 VGPRs, 8 waves per
 // SIMD) gains from 512-element tiles (halo 4 % instead of 8 %: 101 -> 93 us per step with the
 // SGPR cap); the adjoint (117 VGPRs, 4 waves per SIMD) loses (145 -> 151 us): with two
-// 8-wave workgroups per CU each barrier stalls half the CU's waves.
+// 8-wave workgroups per CU each barrier stalls half the CU's waves.  Round 6: 768- and
+// 1024-element forward tiles (fewer tile rounds per launch, 2-3 % less halo) measured 99 and
+// 94 us per step against 88 (profiles/r06/c3w/, patches in profiles/r06/variants/): 12- and
+// 16-wave barriers cost more than the tail they save.
 constexpr int kNLStepW = 2, kNLAdjW = 1;
 
 template <int NP, bool BURG, bool LIM, bool UNI, int MS>
