@@ -99,15 +99,17 @@ def p_flops_per_update(Np):
 def halo_factor(T, H):
   """Lanes issued per useful lane of a tile of T elements whose launch writes T - 2 H."""
   return T / float(T - 2 * H)
-# Profiles of bench configurations (profiles/r05/collect.sh): each directory holds the per-launch
-# PMC traffic of the sweep kernel (pmc_traffic.json) and its SQ passes (sq_summary.json: issued
-# fp64 instructions); a bench line uses the one whose N, K, shape and kernel (instantiation and
-# occupancy target, `sweep_kernel`) match, else reports traffic null
+# Profiles of bench configurations (profiles/r06/collect.sh, profiles/r05/collect.sh): each
+# directory holds the per-launch PMC traffic of the sweep kernel (pmc_traffic.json) and its SQ
+# passes (sq_summary.json: issued fp64 instructions); a bench line uses the first whose N, K,
+# shape and kernel (instantiation and occupancy target, `sweep_kernel`) match, else reports
+# traffic null
 PROFILE_DIRS = {
-    "jumps": [os.path.join(ROOT, "profiles", "r05", d)
-              for d in ("headline", "N1", "N2", "N6", "N8", "c4")],
+    "jumps": ([os.path.join(ROOT, "profiles", "r06", d) for d in ("headline", "N1")] +
+              [os.path.join(ROOT, "profiles", "r05", d)
+               for d in ("headline", "N1", "N2", "N6", "N8", "c4")]),
     "snapshots": [os.path.join(ROOT, "profiles", "r02")],
-    "p": [os.path.join(ROOT, "profiles", "r05", "p")]}
+    "p": [os.path.join(ROOT, "profiles", d, "p") for d in ("r06", "r05")]}
 PROFILE_TRAFFIC_FILE = {"snapshots": "pmc_traffic_snapshots.json"}  # default pmc_traffic.json
 
 
