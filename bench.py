@@ -292,6 +292,50 @@ def cpu_baseline(N, K, nsteps, threads=1, indicator="jump", ics=1, ics_total=1):
           "sample": sample}
 
 
+def cpu_baseline_cport(N, K, nsteps, threads, ics=1, ics_total=1):
+  """The oracle's C restatement (oracle/c/advec_oracle.c: the same LSERK4 forward + discrete
+  adjoint + DWR jump indicator as the numpy oracle, element loops compiled with gcc -O3 and
+  OpenMP, checked against it by tests/test_oracle_cport.py) over `nsteps` forward + adjoint
+  steps at the full N, K on `threads` host threads: a CPU port as one would run it, beside
+  the MATLAB-style numpy restatement.  None when its library is not built."""
+  from oracle import advec as oadv
+  from oracle import cport
+  from oracle import setup1d
+  try:
+    cport.load()
+  except OSError:
+    return None
+  S = setup1d.uniform_setup(N, K, metric="element")
+  mesh = cport.Mesh(S, 2 * np.pi)
+  dt = oadv.bench_dt(S)
+  u0 = setup1d.to_elem_major(np.sin(2 * np.pi * S["x"]))
+  t0 = time.perf_counter()
+  snaps, times = cport.forward_sweep(u0, 0.0, dt, nsteps, mesh, threads=threads)
+  cport.adjoint_sweep(snaps[-1], snaps, times, dt, mesh, threads=threads)
+  el = time.perf_counter() - t0
+  dofs = 2 * (N + 1) * K * nsteps
+  sample = (f"{nsteps} fwd + {nsteps} adj LSERK4 steps (with DWR jump indicator) at N={N}, "
+            f"K={K}, C port of the oracle (gcc -O3, OpenMP), {threads} thread(s), {el:.1f} s")
+  if ics_total > 1:
+    sample += (f"; 1 of the workload's {ics_total} trajectories (time is linear in the "
+               f"trajectory count, so the rate stands for all of them)")
+  return {"value": dofs / el, "unit": "DOF-updates/s", "cores": threads, "kind": "port",
+          "sample": sample}
+
+
+def host_threads():
+  """The host threads a CPU baseline may use: OMP_NUM_THREADS where set (16 on the GPU box),
+  else the process's CPU affinity, at most 16."""
+  env = os.environ.get("OMP_NUM_THREADS")
+  if env and env.isdigit() and int(env) > 0:
+    return int(env)
+  try:
+    n = len(os.sched_getaffinity(0))
+  except (AttributeError, OSError):
+    n = os.cpu_count() or 1
+  return max(1, min(16, n))
+
+
 def cpu_baseline_config3(N, K, nsteps):
   """The oracle's limited Burgers forward step (numpy, one thread) on a bounded sample of
   the config-3 workload.  Forward only: the oracle's adjoint is a coloured-Jacobian checker
@@ -1176,9 +1220,20 @@ def main(argv=None):
   if rank == 0 and world == 1 and not args.no_cpu_baseline:
     cs = args.cpu_steps if not pmode else max(2, args.cpu_steps // 2)
     kw = dict(indicator=args.indicator, ics=min(2, n_total), ics_total=n_total)
-    out["cpu_baseline"] = cpu_baseline(N, K, cs, **kw)
-    if args.ics == 0:
-      out["cpu_baseline_8t"] = cpu_baseline(N, K, cs, threads=8, **kw)
+    numpy_1t = cpu_baseline(N, K, cs, **kw)
+    cport = None
+    if not pmode and args.record == "jumps":
+      # the oracle's C port on the host's cores (the workload's own 20 + 20 steps), and on
+      # one core; the numpy restatement (MATLAB-style whole-array passes) beside them
+      th = host_threads()
+      cport = cpu_baseline_cport(N, K, nsteps, th, ics_total=n_total)
+      if cport is not None and args.ics == 0:
+        out["cpu_baseline_1t"] = cpu_baseline_cport(N, K, nsteps, 1, ics_total=n_total)
+    if cport is not None:
+      out["cpu_baseline"] = cport
+      out["cpu_baseline_numpy"] = numpy_1t
+    else:
+      out["cpu_baseline"] = numpy_1t
   if rank == 0:
     print(json.dumps(out, allow_nan=False), flush=True)
   if world > 1:
