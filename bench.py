@@ -292,7 +292,7 @@ def cpu_baseline(N, K, nsteps, threads=1, indicator="jump", ics=1, ics_total=1):
           "sample": sample}
 
 
-def cpu_baseline_cport(N, K, nsteps, threads, ics=1, ics_total=1):
+def cpu_baseline_cport(N, K, nsteps, threads, ics=1, ics_total=1, min_seconds=2.0):
   """The oracle's C restatement (oracle/c/advec_oracle.c: the same LSERK4 forward + discrete
   adjoint + DWR jump indicator as the numpy oracle, element loops compiled with gcc -O3 and
   OpenMP, checked against it by tests/test_oracle_cport.py) over `nsteps` forward + adjoint
@@ -309,13 +309,19 @@ def cpu_baseline_cport(N, K, nsteps, threads, ics=1, ics_total=1):
   mesh = cport.Mesh(S, 2 * np.pi)
   dt = oadv.bench_dt(S)
   u0 = setup1d.to_elem_major(np.sin(2 * np.pi * S["x"]))
-  t0 = time.perf_counter()
-  snaps, times = cport.forward_sweep(u0, 0.0, dt, nsteps, mesh, threads=threads)
-  cport.adjoint_sweep(snaps[-1], snaps, times, dt, mesh, threads=threads)
-  el = time.perf_counter() - t0
-  dofs = 2 * (N + 1) * K * nsteps
-  sample = (f"{nsteps} fwd + {nsteps} adj LSERK4 steps (with DWR jump indicator) at N={N}, "
-            f"K={K}, C port of the oracle (gcc -O3, OpenMP), {threads} thread(s), {el:.1f} s")
+  # whole sweeps, repeated until min_seconds have passed (a 16-thread sweep takes ~0.3 s)
+  reps, el = 0, 0.0
+  while reps == 0 or el < min_seconds:
+    t0 = time.perf_counter()
+    snaps, times = cport.forward_sweep(u0, 0.0, dt, nsteps, mesh, threads=threads)
+    cport.adjoint_sweep(snaps[-1], snaps, times, dt, mesh, threads=threads)
+    el += time.perf_counter() - t0
+    reps += 1
+    del snaps
+  dofs = 2 * (N + 1) * K * nsteps * reps
+  sample = (f"{reps} x ({nsteps} fwd + {nsteps} adj LSERK4 steps with DWR jump indicator) at "
+            f"N={N}, K={K}, C port of the oracle (gcc -O3, OpenMP), {threads} thread(s), "
+            f"{el:.1f} s")
   if ics_total > 1:
     sample += (f"; 1 of the workload's {ics_total} trajectories (time is linear in the "
                f"trajectory count, so the rate stands for all of them)")
