@@ -69,10 +69,16 @@ def test_bench_p_estimate_line(gpu):
   """--indicator p: the forward keeps snapshots and the estimate runs at order N+1 with the
   prolonged one-step residual -- by default both as ONE dataflow launch (k_psweep, with the
   refine decision); its line carries the same roofline blocks and a CPU baseline of the
-  oracle's p-estimate."""
+  oracle's p-estimate.  (The jump line run first carries the compiled oracle port's.)"""
   out = _run(["--K", "65536", "--steps", "3", "--warmup", "2", "--no-converge",
               "--cpu-steps", "2"])
   assert out["indicator"] == "jump"
+  # the jump line's CPU baseline: the oracle's C port on the host threads and on one, the
+  # numpy oracle beside them (round 6)
+  cb, c1, cn = out["cpu_baseline"], out["cpu_baseline_1t"], out["cpu_baseline_numpy"]
+  assert "C port" in cb["sample"] and cb["kind"] == "port" and cb["cores"] >= 1
+  assert c1["cores"] == 1 and "C port" in c1["sample"] and "numpy" in cn["sample"]
+  assert cb["value"] > 0 and c1["value"] > 0 and cn["value"] > 0
   out = _run(["--K", "65536", "--steps", "3", "--warmup", "2", "--no-converge",
               "--indicator", "p", "--cpu-steps", "2"])
   assert out["indicator"] == "p" and out["config"]["record"] == "snapshots"
