@@ -292,7 +292,8 @@ def cpu_baseline(N, K, nsteps, threads=1, indicator="jump", ics=1, ics_total=1):
           "sample": sample}
 
 
-def cpu_baseline_cport(N, K, nsteps, threads, ics=1, ics_total=1, min_seconds=2.0):
+def cpu_baseline_cport(N, K, nsteps, threads, ics=1, ics_total=1, min_seconds=2.0,
+                       indicator="jump"):
   """The oracle's C restatement (oracle/c/advec_oracle.c: the same LSERK4 forward + discrete
   adjoint + DWR jump indicator as the numpy oracle, element loops compiled with gcc -O3 and
   OpenMP, checked against it by tests/test_oracle_cport.py) over `nsteps` forward + adjoint
@@ -307,25 +308,52 @@ def cpu_baseline_cport(N, K, nsteps, threads, ics=1, ics_total=1, min_seconds=2.
     return None
   S = setup1d.uniform_setup(N, K, metric="element")
   mesh = cport.Mesh(S, 2 * np.pi)
+  pmode = indicator == "p"
+  if pmode:  # the p-enriched estimate: order N+1 operators and the prolongation
+    from oracle import effectivity as oef
+    S_hi = setup1d.uniform_setup(N + 1, K, metric="element")
+    mesh_hi = cport.Mesh(S_hi, 2 * np.pi)
+    P = oef.prolong_matrix(S, S_hi)
   dt = oadv.bench_dt(S)
   u0 = setup1d.to_elem_major(np.sin(2 * np.pi * S["x"]))
-  # whole sweeps, repeated until min_seconds have passed (a 16-thread sweep takes ~0.3 s)
-  reps, el = 0, 0.0
-  while reps == 0 or el < min_seconds:
+  # untimed: one short sweep of the same kind on a small mesh (the first call of each entry
+  # point costs ~0.3-0.6 s on its own: the OpenMP runtime and the library starting up)
+  Kw = 256
+  S_w = setup1d.uniform_setup(N, Kw, metric="element")
+  m_w = cport.Mesh(S_w, 2 * np.pi)
+  w_snaps, w_times = cport.forward_sweep(setup1d.to_elem_major(np.sin(S_w["x"])), 0.0, dt, 2,
+                                         m_w, threads=threads)
+  if pmode:
+    S_wh = setup1d.uniform_setup(N + 1, Kw, metric="element")
+    cport.p_estimate(w_snaps, w_times, dt, cport.Mesh(S_wh, 2 * np.pi), P,
+                     np.zeros(Kw * (N + 2)), N + 1, threads=threads)
+  else:
+    cport.adjoint_sweep(w_snaps[-1], w_snaps, w_times, dt, m_w, threads=threads)
+  # whole sweeps, at least three and until min_seconds have passed (a 16-thread sweep takes
+  # ~0.3 s); the rate is the median sweep's (a first sweep can carry start-up costs)
+  reps, el, laps = 0, 0.0, []
+  while reps < 3 or el < min_seconds:
     t0 = time.perf_counter()
     snaps, times = cport.forward_sweep(u0, 0.0, dt, nsteps, mesh, threads=threads)
-    cport.adjoint_sweep(snaps[-1], snaps, times, dt, mesh, threads=threads)
-    el += time.perf_counter() - t0
+    if pmode:
+      g_hi = (P @ snaps[-1].reshape(K, N + 1).T).T.ravel()  # P u^N, element-major
+      cport.p_estimate(snaps, times, dt, mesh_hi, P, g_hi, N + 1, threads=threads)
+    else:
+      cport.adjoint_sweep(snaps[-1], snaps, times, dt, mesh, threads=threads)
+    laps.append(time.perf_counter() - t0)
+    el += laps[-1]
     reps += 1
     del snaps
-  dofs = 2 * (N + 1) * K * nsteps * reps
-  sample = (f"{reps} x ({nsteps} fwd + {nsteps} adj LSERK4 steps with DWR jump indicator) at "
-            f"N={N}, K={K}, C port of the oracle (gcc -O3, OpenMP), {threads} thread(s), "
-            f"{el:.1f} s")
+  lap = float(np.median(laps))
+  dofs = 2 * (N + 1) * K * nsteps
+  what = "p-enriched DWR estimate" if pmode else "DWR jump indicator"
+  sample = (f"median of {reps} sweeps of {nsteps} fwd + {nsteps} adj LSERK4 steps with {what} "
+            f"at N={N}, K={K}, C port of the oracle (gcc -O3, OpenMP), {threads} thread(s), "
+            f"{lap:.2f} s per sweep")
   if ics_total > 1:
     sample += (f"; 1 of the workload's {ics_total} trajectories (time is linear in the "
                f"trajectory count, so the rate stands for all of them)")
-  return {"value": dofs / el, "unit": "DOF-updates/s", "cores": threads, "kind": "port",
+  return {"value": dofs / lap, "unit": "DOF-updates/s", "cores": threads, "kind": "port",
           "sample": sample}
 
 
@@ -1228,13 +1256,14 @@ def main(argv=None):
     kw = dict(indicator=args.indicator, ics=min(2, n_total), ics_total=n_total)
     numpy_1t = cpu_baseline(N, K, cs, **kw)
     cport = None
-    if not pmode and args.record == "jumps":
+    if pmode or args.record == "jumps":
       # the oracle's C port on the host's cores (the workload's own 20 + 20 steps), and on
       # one core; the numpy restatement (MATLAB-style whole-array passes) beside them
       th = host_threads()
-      cport = cpu_baseline_cport(N, K, nsteps, th, ics_total=n_total)
+      ckw = dict(ics_total=n_total, indicator=args.indicator)
+      cport = cpu_baseline_cport(N, K, nsteps, th, **ckw)
       if cport is not None and args.ics == 0:
-        out["cpu_baseline_1t"] = cpu_baseline_cport(N, K, nsteps, 1, ics_total=n_total)
+        out["cpu_baseline_1t"] = cpu_baseline_cport(N, K, nsteps, 1, **ckw)
     if cport is not None:
       out["cpu_baseline"] = cport
       out["cpu_baseline_numpy"] = numpy_1t

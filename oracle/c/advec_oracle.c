@@ -6,6 +6,11 @@
  *   oc_forward_sweep  -- oracle/advec.py forward_sweep: the LSERK4 stage loop of
  *                        utils/One_code.mlx:120-139 over AdvecRHS1D (utils/AdvecRHS1D.m:9-19,
  *                        central flux alpha = 1, inflow uin = -sin(a t), du(mapO) = 0).
+ *   oc_p_estimate     -- oracle/effectivity.py p_estimate (inflow uin = -sin(a t)): the
+ *                        order-(N+1) adjoint from the terminal weight g (adj_march.m:103-117
+ *                        at order N+1, MAIN.m:32-34) paired with the prolonged one-step
+ *                        residual R^n = P u^{n+1} - S_{N+1}(P u^n, t_n): eta -= w^{n+1}.R^n
+ *                        (summed here from the last step back, the oracle sums forward).
  *   oc_adjoint_sweep  -- oracle/adjoint.py adjoint_sweep (src = 0): eta += dt sum_i w^{n+1}
  *                        R(u^{n+1}, t_{n+1}) with R = LIFT (Fscale .* du) (AdvecRHS1D.m:19),
  *                        then w^n = S^T w^{n+1} through the reversed stages
@@ -270,4 +275,85 @@ int oc_adjoint_sweep(int np, long K, const double* dr, const double* lift, const
   free(t);
   free(zc);
   return 0;
+}
+
+/* out = P u element by element (oracle/effectivity.py prolong_matrix: order-N nodal values to
+ * the order-(N+1) LGL nodes); P row-major nph x npl. */
+static void prolong(int npl, int nph, long K, const double* P, const double* u, double* out) {
+#pragma omp parallel for schedule(static)
+  for (long k = 0; k < K; ++k) {
+    const double* uk = u + k * npl;
+    double* ok = out + k * nph;
+    for (int i = 0; i < nph; ++i) {
+      double d = 0.0;
+      for (int j = 0; j < npl; ++j) d += P[i * npl + j] * uk[j];
+      ok[i] = d;
+    }
+  }
+}
+
+/* snaps: u^0..u^nsteps at order N (npl nodes); the operators are the order-(N+1) mesh's (nph
+ * nodes; the same per-element metric); w: the terminal weight g at order N+1 on entry, w^0 on
+ * exit; eta (K) assigned.  times: t_0..t_nsteps. */
+int oc_p_estimate(int npl, int nph, long K, const double* dr, const double* lift,
+                  const double* rx, const double* fsl, const double* fsr, const double* P,
+                  double a, double dt, int nsteps, const double* rk, const double* times,
+                  const double* snaps, double* w, double* eta) {
+  if (npl < 1 || nph < 1 || nph > OC_MAXNP || K < 1 || nsteps < 0) return 1;
+  const oc_mesh m = {nph, K, dr, lift, rx, fsl, fsr, a};
+  const long nl = (long)npl * K, nh = (long)nph * K;
+  double* pa = (double*)malloc(sizeof(double) * (size_t)nh);
+  double* pb = (double*)malloc(sizeof(double) * (size_t)nh);
+  double* s1 = (double*)malloc(sizeof(double) * (size_t)nh);
+  double* s2 = (double*)malloc(sizeof(double) * (size_t)nh);
+  double* res = (double*)malloc(sizeof(double) * (size_t)nh);
+  double* lr = (double*)malloc(sizeof(double) * (size_t)nh);
+  double* zc = (double*)malloc(sizeof(double) * (size_t)(2 * K));
+  int rc = 0;
+  if (!pa || !pb || !s1 || !s2 || !res || !lr || !zc) {
+    rc = 2;
+    goto done;
+  }
+  par_zero(eta, K);
+  for (int step = nsteps - 1; step >= 0; --step) {
+    /* R = P u^{n+1} - S_{N+1}(P u^n, t_n): the stage loop of oracle/advec.py lserk4_step */
+    prolong(npl, nph, K, P, snaps + (long)(step + 1) * nl, pa);
+    prolong(npl, nph, K, P, snaps + (long)step * nl, pb);
+    par_zero(res, nh);
+    const double* u = pb;
+    for (int s = 0; s < 5; ++s) {
+      double* dst = (s % 2 == 0) ? s1 : s2;
+      stage(&m, u, -sin(a * (times[step] + rk[10 + s] * dt)), rk[s], rk[5 + s], dt, res, dst);
+      u = dst;
+    }
+    /* eta -= w^{n+1} . R (u = s1: the step's result) */
+#pragma omp parallel for schedule(static)
+    for (long k = 0; k < K; ++k) {
+      double c = 0.0;
+      for (int i = 0; i < nph; ++i) c += w[k * nph + i] * (pa[k * nph + i] - u[k * nph + i]);
+      eta[k] = eta[k] - c;
+    }
+    /* w^n = S_{N+1}^T w^{n+1} (oracle/adjoint.py adjoint_step) */
+    par_zero(lr, nh);
+    for (int s = 4; s >= 0; --s) {
+      const double A = rk[s], B = rk[5 + s];
+#pragma omp parallel for schedule(static)
+      for (long q = 0; q < nh; ++q) lr[q] = lr[q] + B * w[q];
+      lin_t(&m, lr, s2, zc);
+#pragma omp parallel for schedule(static)
+      for (long q = 0; q < nh; ++q) {
+        w[q] = w[q] + dt * s2[q];
+        lr[q] = A * lr[q];
+      }
+    }
+  }
+done:
+  free(pa);
+  free(pb);
+  free(s1);
+  free(s2);
+  free(res);
+  free(lr);
+  free(zc);
+  return rc;
 }

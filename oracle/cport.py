@@ -1,9 +1,9 @@
 """ctypes wrapper of oracle/c/advec_oracle.c -- TEST INFRASTRUCTURE ONLY (oracle/__init__.py).
 
-A compiled (gcc -O3, OpenMP) restatement of :func:`oracle.advec.forward_sweep` and
-:func:`oracle.adjoint.adjoint_sweep` (source 0, inflow ``INFLOW_A``) for bench.py's CPU
-baseline: the same algorithm as the numpy oracle, written the way a CPU port would run it
-(element loops, all host cores).  tests/test_oracle_cport.py checks it against the numpy
+A compiled (gcc -O3, OpenMP) restatement of :func:`oracle.advec.forward_sweep`,
+:func:`oracle.adjoint.adjoint_sweep` (source 0) and :func:`oracle.effectivity.p_estimate`
+(inflow ``INFLOW_A``) for bench.py's CPU baseline: the same algorithm as the numpy oracle,
+written the way a CPU port would run it (element loops, all host cores).  tests/test_oracle_cport.py checks it against the numpy
 oracle.  :func:`build` compiles it into ``oracle/liboracle_advec.so`` (git-ignored; it travels
 to the GPU box with the tree like the product library).
 """
@@ -47,6 +47,9 @@ def load():
     lib.oc_adjoint_sweep.restype = i32
     lib.oc_adjoint_sweep.argtypes = [i32, i64, dp, dp, dp, dp, dp, f64, f64, i32, dp, dp, dp,
                                      dp, dp]
+    lib.oc_p_estimate.restype = i32
+    lib.oc_p_estimate.argtypes = [i32, i32, i64, dp, dp, dp, dp, dp, dp, f64, f64, i32, dp, dp,
+                                  dp, dp, dp]
     lib.oc_set_threads.restype = None
     lib.oc_set_threads.argtypes = [i32]
     _lib = lib
@@ -108,3 +111,23 @@ def adjoint_sweep(wT, snaps, times, dt, mesh, threads=1):
   if rc:
     raise RuntimeError(f"oc_adjoint_sweep failed ({rc})")
   return w, eta
+
+
+def p_estimate(snaps, times, dt, mesh_hi, P, g_hi, npl, threads=1):
+  """oracle/effectivity.py p_estimate (inflow INFLOW_A) on element-major fields: snaps
+  (nsteps+1, K npl) at order N, g_hi the order-(N+1) terminal weight, P (nph, npl), mesh_hi
+  the order-(N+1) setup's Mesh.  Returns (eta (K,), w^0 at order N+1)."""
+  lib = load()
+  lib.oc_set_threads(int(threads))
+  w = np.array(g_hi, dtype=np.float64, copy=True)
+  eta = np.empty(mesh_hi.K)
+  tt = np.ascontiguousarray(times, dtype=np.float64)
+  sn = np.ascontiguousarray(snaps)
+  Pc = np.ascontiguousarray(P, dtype=np.float64)
+  rc = lib.oc_p_estimate(int(npl), mesh_hi.Np, mesh_hi.K, _p(mesh_hi.dr), _p(mesh_hi.lift),
+                         _p(mesh_hi.rx), _p(mesh_hi.fsl), _p(mesh_hi.fsr), _p(Pc), mesh_hi.a,
+                         float(dt), int(len(snaps) - 1), _p(mesh_hi.rk), _p(tt), _p(sn), _p(w),
+                         _p(eta))
+  if rc:
+    raise RuntimeError(f"oc_p_estimate failed ({rc})")
+  return eta, w

@@ -8,6 +8,7 @@ import pytest
 from oracle import adjoint as oadj
 from oracle import advec as oadv
 from oracle import cport
+from oracle import effectivity as oef
 from oracle import setup1d
 
 A = 2.0 * np.pi
@@ -77,3 +78,22 @@ def test_cport_rejects_a_nodal_metric(built):
     pytest.skip("this mesh's nodal metric happens to be constant per element")
   with pytest.raises(ValueError):
     cport.Mesh(S, A)
+
+
+@pytest.mark.parametrize("N,K,nsteps,threads", [(4, 200, 8, 1), (2, 150, 6, 3), (6, 80, 4, 2)])
+def test_cport_p_estimate_equals_numpy_oracle(built, N, K, nsteps, threads):
+  """The p-enriched estimate (order-(N+1) adjoint from P u^N, prolonged one-step residual)
+  against oracle/effectivity.py p_estimate on the same order-N snapshots."""
+  rng = np.random.default_rng(7 * N + K)
+  S = setup1d.uniform_setup(N, K, metric="element")
+  S_hi = setup1d.uniform_setup(N + 1, K, metric="element")
+  dt = oadv.bench_dt(S)
+  u0 = np.sin(2 * np.pi * S["x"]) + 0.1 * rng.standard_normal(S["x"].shape)
+  snaps, times = oadv.forward_sweep(u0, 0.0, dt, nsteps, A, S)
+  P = oef.prolong_matrix(S, S_hi)
+  eta, w0 = oef.p_estimate(snaps, times, dt, A, S, S_hi, P @ snaps[-1], inflow=oadv.INFLOW_A)
+  esn = np.stack([setup1d.to_elem_major(u) for u in snaps])
+  ceta, cw0 = cport.p_estimate(esn, times, dt, cport.Mesh(S_hi, A), P,
+                               setup1d.to_elem_major(P @ snaps[-1]), N + 1, threads=threads)
+  close(ceta, eta, "eta")
+  close(cw0, setup1d.to_elem_major(w0), "w^0")
