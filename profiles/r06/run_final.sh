@@ -1,7 +1,7 @@
 # Round 6, final: the whole GPU suite + smoke on the committed tree, then the driver's bench
 # command and the config-3 / p lines
 set -o pipefail
-out=gpurun_out/r06/final; mkdir -p $out
+out=gpurun_out/r06/${FINAL_TAG:-final}; mkdir -p $out
 timeout -k 10 1000 python -u -m pytest -q --timeout 500 --timeout-method thread -m gpu tests/ > $out/pytest.log 2>&1; rc=$?
 tail -2 $out/pytest.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error" $out/pytest.log | head; exit 1; }
@@ -13,7 +13,7 @@ timeout -k 10 300 python bench.py --indicator p > $out/bench_p.json 2> $out/benc
 python3 - <<'PY'
 import json
 for f in ("bench", "bench_c3", "bench_p"):
-  d = json.loads(open(f"gpurun_out/r06/final/{f}.json").read().strip().splitlines()[-1])
+  d = json.loads(open(f"gpurun_out/r06/{__import__('os').environ.get('FINAL_TAG', 'final')}/{f}.json").read().strip().splitlines()[-1])
   r = d["roofline"]
   print(f, "%.4g" % d["value"], r.get("bound"), "frac %.3f" % r["frac"], "traffic", r.get("traffic"), "cpu", d.get("cpu_baseline", {}).get("value"))
 PY
